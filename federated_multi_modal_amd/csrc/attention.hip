@@ -1,0 +1,398 @@
+// Multi-head self-attention core of both CLIP towers: the SDPA that
+// nn.MultiheadAttention(need_weights=False) runs inside ResidualAttentionBlock_MaPLe.attention
+// (clip/model.py:303-305), with the text tower's additive causal mask (clip/model.py:679-685).
+//
+// Layout: qkv is the in-projection output [N*L, 3*D] (row n*L+l; q|k|v blocks of D = H*64
+// columns, head h at columns h*64..h*64+63 of each block), out / dout are [N*L, D].
+// head_dim = 64, L <= 256 (vision 199, text 77) so a whole head's K and V fit in LDS: no online
+// rescaling is needed.  Numerics follow torch's CPU flash kernel for fp16: scores in fp32,
+// scale 1/8 applied in fp32, P = exp(s - rowmax) in fp32, row sum from the fp32 P, P rounded to
+// fp16 for the PV product (fp32 accumulate), out = fp16(acc * (1/sum)).
+//
+// MFMA v_mfma_f32_16x16x32_f16 throughout, issued so that the reduction axis of each product
+// lands where the next product needs it:
+//   fwd:  S^T = K Q^T  -> each lane owns one query, 4 keys per 16-key tile (row max/sum by two
+//         shuffles); O^T = V^T P^T takes P straight from the accumulators (keys permuted
+//         consistently in both operands), V^T fragments by ds_read_b64_tr_b16 from the
+//         row-major LDS image; each lane then holds 4 consecutive output columns (8-B stores).
+//   bwd:  dK/dV kernel (grid over 64-key blocks, Q and dO for the head in LDS) and dQ kernel
+//         (grid over 64-query blocks, K and V in LDS); P is recomputed from the saved LSE.
+// LDS images are [rows][64] fp16 with the 16-byte chunk XOR swizzle chunk ^ (row & 7).
+#include "mf_common.h"
+
+namespace {
+
+MF_DEV int sw_off(int row, int col) {  // element offset in a swizzled [rows][64] fp16 image
+  return row * 64 + ((((col >> 3) ^ (row & 7))) << 3) + (col & 7);
+}
+
+// 16 lanes of a group read rows r0..r0+3 x cols c0..c0+15; lane i gets column c0+i.
+MF_DEV f16x4 tr_read(const f16* img, int r0, int c0, int lane) {
+  const int ii = lane & 15;
+  const int row = r0 + (ii >> 2);
+  const int col = c0 + 4 * (ii & 3);
+  const f16* p = img + sw_off(row, col);
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+  return __builtin_bit_cast(f16x4, v);
+}
+
+MF_DEV f16x8 cat8(f16x4 a, f16x4 b) {
+  return (f16x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+MF_DEV f16x8 ld_frag(const f16* img, int row, int chunk) {
+  return *(const f16x8*)(img + row * 64 + ((chunk ^ (row & 7)) << 3));
+}
+
+// Stage rows [0, LP) of one head (column offset col0 inside the qkv-like row) into a swizzled
+// LDS image; rows >= L are zero.
+template <int LP>
+MF_DEV void stage_rows(f16* img, const f16* base, int64_t ld, int L, int col0) {
+  for (int idx = threadIdx.x; idx < LP * 8; idx += blockDim.x) {
+    const int row = idx >> 3, c = idx & 7;
+    f16x8 v = {};
+    if (row < L) v = *(const f16x8*)(base + (int64_t)row * ld + col0 + c * 8);
+    *(f16x8*)(img + row * 64 + ((c ^ (row & 7)) << 3)) = v;
+  }
+}
+
+constexpr float kScale = 0.125f;  // 1/sqrt(64), SDPA default
+
+// ---------------------------------------------------------------------------------------------
+template <int LKP, bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
+                                                      f16* __restrict__ out, int64_t ld_out,
+                                                      float* __restrict__ lse, int ld_lse, int L, int H) {
+  constexpr int NKT = LKP / 16;
+  __shared__ __attribute__((aligned(16))) f16 sK[LKP * 64];
+  __shared__ __attribute__((aligned(16))) f16 sV[LKP * 64];
+  const int D = H * 64;
+  const int nh = blockIdx.x, n = nh / H, h = nh % H;
+  const f16* base = qkv + (int64_t)n * L * ld_qkv;
+  stage_rows<LKP>(sK, base, ld_qkv, L, D + h * 64);
+  stage_rows<LKP>(sV, base, ld_qkv, L, 2 * D + h * 64);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q0 = blockIdx.y * 64 + w * 16;
+  if (q0 >= L) return;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int q = q0 + fr;
+  const int qc = q < L ? q : L - 1;
+  f16x8 qf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) qf[s] = *(const f16x8*)(base + (int64_t)qc * ld_qkv + h * 64 + 32 * s + 8 * fg);
+
+  const int kt_end = CAUSAL ? min(NKT, (q0 + 16 + 15) / 16) : NKT;
+  f32x4 sacc[NKT];
+  float m = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (kt < kt_end) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        f16x8 kf = ld_frag(sK, kt * 16 + fr, 4 * s + fg);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[s], acc, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int key = kt * 16 + 4 * fg + i;
+      float v = acc[i] * kScale;
+      if (key >= L || (CAUSAL && key > q) || kt >= kt_end) v = -INFINITY;
+      acc[i] = v;
+      m = fmaxf(m, v);
+    }
+    sacc[kt] = acc;
+  }
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float l = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float p = __expf(sacc[kt][i] - m);
+      sacc[kt][i] = p;
+      l += p;
+    }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+
+  f32x4 oacc[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) oacc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < NKT / 2; ++ks) {
+    if (CAUSAL && 2 * ks >= kt_end) break;
+    f16x8 pf = {(f16)sacc[2 * ks][0], (f16)sacc[2 * ks][1], (f16)sacc[2 * ks][2], (f16)sacc[2 * ks][3],
+                (f16)sacc[2 * ks + 1][0], (f16)sacc[2 * ks + 1][1], (f16)sacc[2 * ks + 1][2],
+                (f16)sacc[2 * ks + 1][3]};
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f16x8 vf = cat8(tr_read(sV, 32 * ks + 4 * fg, 16 * dt, lane), tr_read(sV, 32 * ks + 16 + 4 * fg, 16 * dt, lane));
+      oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf, oacc[dt], 0, 0, 0);
+    }
+  }
+  if (q < L) {
+    const float inv = 1.0f / l;
+    f16* orow = out + ((int64_t)n * L + q) * ld_out + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f16x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = (f16)(oacc[dt][i] * inv);
+      *(f16x4*)(orow + 16 * dt + 4 * fg) = o;
+    }
+    if (fg == 0) lse[(int64_t)nh * ld_lse + q] = m + __logf(l);
+  }
+}
+
+// Dq[nh][q] = sum_d dO[q][d] * O[q][d] (fp32) ------------------------------------------------
+__global__ void attn_bwd_dot_kernel(const f16* __restrict__ out, int64_t ld_out, const f16* __restrict__ dout,
+                                    int64_t ld_dout, float* __restrict__ dq_dot, int ld_lse, int N, int L, int H) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over N*H*L
+  if (t >= (int64_t)N * H * L) return;
+  const int q = t % L;
+  const int nh = t / L;
+  const int n = nh / H, h = nh % H;
+  const f16* o = out + ((int64_t)n * L + q) * ld_out + h * 64;
+  const f16* d = dout + ((int64_t)n * L + q) * ld_dout + h * 64;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    f16x8 a = *(const f16x8*)(o + 8 * c), b = *(const f16x8*)(d + 8 * c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += (float)a[e] * (float)b[e];
+  }
+  dq_dot[(int64_t)nh * ld_lse + q] = s;
+}
+
+// dK, dV: one workgroup per (n, h, 64-key block); each wave 16 keys, loops over all queries ----
+template <int LQP, bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
+                                                          const f16* __restrict__ dout, int64_t ld_dout,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ dq_dot, int ld_lse,
+                                                          f16* __restrict__ dqkv, int64_t ld_dqkv, int L, int H) {
+  __shared__ __attribute__((aligned(16))) f16 sQ[LQP * 64];
+  __shared__ __attribute__((aligned(16))) f16 sdO[LQP * 64];
+  __shared__ float sL[LQP];
+  __shared__ float sD[LQP];
+  const int D = H * 64;
+  const int nh = blockIdx.x, n = nh / H, h = nh % H;
+  const f16* base = qkv + (int64_t)n * L * ld_qkv;
+  stage_rows<LQP>(sQ, base, ld_qkv, L, h * 64);
+  stage_rows<LQP>(sdO, dout + (int64_t)n * L * ld_dout, ld_dout, L, h * 64);
+  for (int i = threadIdx.x; i < LQP; i += blockDim.x) {
+    sL[i] = i < L ? lse[(int64_t)nh * ld_lse + i] : INFINITY;
+    sD[i] = i < L ? dq_dot[(int64_t)nh * ld_lse + i] : 0.f;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k0 = blockIdx.y * 64 + w * 16;
+  if (k0 >= L) return;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int key = k0 + fr;
+  const int kc = key < L ? key : L - 1;
+  f16x8 kf[2], vf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    kf[s] = *(const f16x8*)(base + (int64_t)kc * ld_qkv + D + h * 64 + 32 * s + 8 * fg);
+    vf[s] = *(const f16x8*)(base + (int64_t)kc * ld_qkv + 2 * D + h * 64 + 32 * s + 8 * fg);
+  }
+  f32x4 dv[4], dk[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dv[dt] = dk[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int qp = 0; qp < LQP / 32; ++qp) {
+    if (CAUSAL && 32 * qp + 31 < k0) continue;  // every query < every key of this wave
+    f16x8 pf, dsf;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int qt = 2 * qp + a;
+      f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, pacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        f16x8 qfr = ld_frag(sQ, qt * 16 + fr, 4 * s + fg);
+        f16x8 ofr = ld_frag(sdO, qt * 16 + fr, 4 * s + fg);
+        sacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(qfr, kf[s], sacc, 0, 0, 0);
+        pacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ofr, vf[s], pacc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qq = qt * 16 + 4 * fg + i;
+        const bool valid = key < L && qq < L && !(CAUSAL && key > qq);
+        const float p = valid ? __expf(sacc[i] * kScale - sL[qq]) : 0.f;
+        const float ds = p * (pacc[i] - sD[qq]);
+        pf[a * 4 + i] = (f16)p;
+        dsf[a * 4 + i] = (f16)ds;
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f16x8 ao = cat8(tr_read(sdO, 32 * qp + 4 * fg, 16 * dt, lane), tr_read(sdO, 32 * qp + 16 + 4 * fg, 16 * dt, lane));
+      dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ao, pf, dv[dt], 0, 0, 0);
+      f16x8 aq = cat8(tr_read(sQ, 32 * qp + 4 * fg, 16 * dt, lane), tr_read(sQ, 32 * qp + 16 + 4 * fg, 16 * dt, lane));
+      dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aq, dsf, dk[dt], 0, 0, 0);
+    }
+  }
+  if (key < L) {
+    f16* row = dqkv + ((int64_t)n * L + key) * ld_dqkv + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f16x4 ok, ov;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ok[i] = (f16)(dk[dt][i] * kScale);
+        ov[i] = (f16)dv[dt][i];
+      }
+      *(f16x4*)(row + D + 16 * dt + 4 * fg) = ok;
+      *(f16x4*)(row + 2 * D + 16 * dt + 4 * fg) = ov;
+    }
+  }
+}
+
+// dQ: one workgroup per (n, h, 64-query block); each wave 16 queries, loops over all keys -------
+template <int LKP, bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
+                                                         const f16* __restrict__ dout, int64_t ld_dout,
+                                                         const float* __restrict__ lse,
+                                                         const float* __restrict__ dq_dot, int ld_lse,
+                                                         f16* __restrict__ dqkv, int64_t ld_dqkv, int L, int H) {
+  constexpr int NKT = LKP / 16;
+  __shared__ __attribute__((aligned(16))) f16 sK[LKP * 64];
+  __shared__ __attribute__((aligned(16))) f16 sV[LKP * 64];
+  const int D = H * 64;
+  const int nh = blockIdx.x, n = nh / H, h = nh % H;
+  const f16* base = qkv + (int64_t)n * L * ld_qkv;
+  stage_rows<LKP>(sK, base, ld_qkv, L, D + h * 64);
+  stage_rows<LKP>(sV, base, ld_qkv, L, 2 * D + h * 64);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q0 = blockIdx.y * 64 + w * 16;
+  if (q0 >= L) return;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int q = q0 + fr;
+  const int qc = q < L ? q : L - 1;
+  f16x8 qf[2], of[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    qf[s] = *(const f16x8*)(base + (int64_t)qc * ld_qkv + h * 64 + 32 * s + 8 * fg);
+    of[s] = *(const f16x8*)(dout + ((int64_t)n * L + qc) * ld_dout + h * 64 + 32 * s + 8 * fg);
+  }
+  const float lq = lse[(int64_t)nh * ld_lse + qc];
+  const float dq_d = dq_dot[(int64_t)nh * ld_lse + qc];
+  f32x4 dq[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dq[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < NKT / 2; ++ks) {
+    if (CAUSAL && 32 * ks > q0 + 15) break;
+    f16x8 dsf;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int kt = 2 * ks + a;
+      f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, pacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        f16x8 kfr = ld_frag(sK, kt * 16 + fr, 4 * s + fg);
+        f16x8 vfr = ld_frag(sV, kt * 16 + fr, 4 * s + fg);
+        sacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(kfr, qf[s], sacc, 0, 0, 0);
+        pacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(vfr, of[s], pacc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = kt * 16 + 4 * fg + i;
+        const bool valid = key < L && q < L && !(CAUSAL && key > q);
+        const float p = valid ? __expf(sacc[i] * kScale - lq) : 0.f;
+        dsf[a * 4 + i] = (f16)(p * (pacc[i] - dq_d));
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f16x8 ak = cat8(tr_read(sK, 32 * ks + 4 * fg, 16 * dt, lane), tr_read(sK, 32 * ks + 16 + 4 * fg, 16 * dt, lane));
+      dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ak, dsf, dq[dt], 0, 0, 0);
+    }
+  }
+  if (q < L) {
+    f16* row = dqkv + ((int64_t)n * L + q) * ld_dqkv + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f16x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = (f16)(dq[dt][i] * kScale);
+      *(f16x4*)(row + 16 * dt + 4 * fg) = o;
+    }
+  }
+}
+
+#define MF_ATTN_DISPATCH(LP, CALL)                         \
+  switch (LP) {                                            \
+    case 32: CALL(32); break;                              \
+    case 64: CALL(64); break;                              \
+    case 96: CALL(96); break;                              \
+    case 128: CALL(128); break;                            \
+    case 160: CALL(160); break;                            \
+    case 192: CALL(192); break;                            \
+    case 224: CALL(224); break;                            \
+    case 256: CALL(256); break;                            \
+    default: return mf_set_error("attention: bad padded length", -1); \
+  }
+
+inline int padded_len(int L) { return ((L + 31) / 32) * 32; }
+
+}  // namespace
+
+extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* lse, int ld_lse,
+                                int N, int L, int H, int causal, void* stream) {
+  if (N <= 0) return 0;
+  if (L <= 0 || L > 256) return mf_set_error("mf_attention_fwd: 0 < L <= 256 required", -1);
+  if (ld_lse < L || (ld_qkv % 8) || (ld_out % 4)) return mf_set_error("mf_attention_fwd: bad strides", -1);
+  const int LP = padded_len(L);
+  dim3 grid(N * H, (L + 63) / 64);
+  hipStream_t st = (hipStream_t)stream;
+#define CALLF(P)                                                                                            \
+  if (causal)                                                                                               \
+    attn_fwd_kernel<P, true><<<grid, 256, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); \
+  else                                                                                                      \
+    attn_fwd_kernel<P, false><<<grid, 256, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H);
+  MF_ATTN_DISPATCH(LP, CALLF)
+#undef CALLF
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_attention_bwd(const void* qkv, int64_t ld_qkv, const void* out, int64_t ld_out, const void* dout,
+                                int64_t ld_dout, const float* lse, float* dq_dot_ws, int ld_lse, void* dqkv,
+                                int64_t ld_dqkv, int N, int L, int H, int causal, void* stream) {
+  if (N <= 0) return 0;
+  if (L <= 0 || L > 256) return mf_set_error("mf_attention_bwd: 0 < L <= 256 required", -1);
+  if (ld_lse < L || (ld_qkv % 8) || (ld_dout % 8) || (ld_dqkv % 4)) return mf_set_error("mf_attention_bwd: bad strides", -1);
+  const int LP = padded_len(L);
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t tot = (int64_t)N * H * L;
+  attn_bwd_dot_kernel<<<(tot + 255) / 256, 256, 0, st>>>((const f16*)out, ld_out, (const f16*)dout, ld_dout,
+                                                        dq_dot_ws, ld_lse, N, L, H);
+  MF_CHECK_LAUNCH();
+  dim3 grid(N * H, (L + 63) / 64);
+#define CALLB(P)                                                                                                 \
+  if (causal) {                                                                                                  \
+    attn_bwd_dkv_kernel<P, true><<<grid, 256, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)dout, ld_dout, lse,    \
+                                                       dq_dot_ws, ld_lse, (f16*)dqkv, ld_dqkv, L, H);              \
+    attn_bwd_dq_kernel<P, true><<<grid, 256, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)dout, ld_dout, lse,     \
+                                                      dq_dot_ws, ld_lse, (f16*)dqkv, ld_dqkv, L, H);               \
+  } else {                                                                                                       \
+    attn_bwd_dkv_kernel<P, false><<<grid, 256, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)dout, ld_dout, lse,   \
+                                                        dq_dot_ws, ld_lse, (f16*)dqkv, ld_dqkv, L, H);             \
+    attn_bwd_dq_kernel<P, false><<<grid, 256, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)dout, ld_dout, lse,    \
+                                                       dq_dot_ws, ld_lse, (f16*)dqkv, ld_dqkv, L, H);              \
+  }
+  MF_ATTN_DISPATCH(LP, CALLB)
+#undef CALLB
+  MF_CHECK_LAUNCH();
+  return 0;
+}

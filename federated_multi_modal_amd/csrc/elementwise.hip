@@ -1,0 +1,339 @@
+// Byte-moving and small kernels around the MaPLe towers (all HBM- or latency-bound):
+//   * patch im2col (K1 operand; image fp32 -> fp16 cast as in trainers/maple.py:336)
+//   * vision token assembly: class token, patches, +pos (fp16 add), shared ctx (clip/model.py:522-538)
+//   * text prompt assembly: prefix | ctx | suffix, +pos (trainers/maple.py:152-166, :54)
+//   * deep-prompt inject and its batch reduction backward (clip/model.py:320-349)
+//   * fp16 transpose (dW operands), fp16 column sums (bias grads)
+//   * small linears of the prompt learner (trainers/maple.py:111-131,194-215)
+#include "mf_common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- im2col for the 16x16/16 conv
+// out[b*G*G + py*G + px][c*P*P + kh*P + kw] = img[b][c][py*P+kh][px*P+kw]   (P = 16, G = R/P)
+template <typename TIn>
+__global__ void im2col_kernel(const TIn* __restrict__ img, f16* __restrict__ out, int B, int R, int P) {
+  const int G = R / P;
+  const int K = 3 * P * P;
+  const int chunks_per_row = K / 8;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)B * G * G * chunks_per_row;
+  if (t >= total) return;
+  const int ch = t % chunks_per_row;
+  const int64_t prow = t / chunks_per_row;
+  const int b = prow / (G * G), pp = prow % (G * G);
+  const int py = pp / G, px = pp % G;
+  const int k = ch * 8;
+  const int c = k / (P * P), kh = (k / P) % P, kw = k % P;
+  const TIn* src = img + (((int64_t)b * 3 + c) * R + (py * P + kh)) * R + px * P + kw;
+  f16x8 v;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (f16)src[e];
+  *(f16x8*)(out + prow * K + k) = v;
+}
+
+// ---------------------------------------------------------------- vision token assembly
+// x[b, 0]      = fp16(fp16(class_emb) + fp16(pos[0]))
+// x[b, 1+p]    = fp16(patch[b, p] + fp16(pos[1+p]))
+// x[b, G2+1+j] = shared_ctx[j]  (j < n_ctx)
+__global__ void vision_assemble_kernel(const f16* __restrict__ patch, const float* __restrict__ cls,
+                                       const float* __restrict__ pos, const f16* __restrict__ shared_ctx,
+                                       f16* __restrict__ x, int B, int G2, int n_ctx, int D) {
+  const int L = G2 + 1 + n_ctx;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over B*L*D/4
+  const int64_t total = (int64_t)B * L * (D / 4);
+  if (t >= total) return;
+  const int d = (t % (D / 4)) * 4;
+  const int64_t row = t / (D / 4);
+  const int l = row % L, b = row / L;
+  f16x4 o;
+  if (l == 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (f16)(r16(cls[d + e]) + r16(pos[d + e]));
+  } else if (l <= G2) {
+    f16x4 p = *(const f16x4*)(patch + ((int64_t)b * G2 + (l - 1)) * D + d);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (f16)((float)p[e] + r16(pos[(int64_t)l * D + d + e]));
+  } else {
+    o = *(const f16x4*)(shared_ctx + (int64_t)(l - G2 - 1) * D + d);
+  }
+  *(f16x4*)(x + row * D + d) = o;
+}
+
+// ---------------------------------------------------------------- text prompt assembly
+// x[k, l] = fp16(src[k,l] + fp16(pos[l])), src = prefix (l=0) | ctx (1..n_ctx) | suffix
+__global__ void text_assemble_kernel(const f16* __restrict__ prefix, const f16* __restrict__ ctx,
+                                     const f16* __restrict__ suffix, const float* __restrict__ pos,
+                                     f16* __restrict__ x, int K, int L, int n_ctx, int D) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)K * L * (D / 4);
+  if (t >= total) return;
+  const int d = (t % (D / 4)) * 4;
+  const int64_t row = t / (D / 4);
+  const int l = row % L, k = row / L;
+  const f16* src;
+  if (l == 0)
+    src = prefix + (int64_t)k * D;
+  else if (l <= n_ctx)
+    src = ctx + (int64_t)(l - 1) * D;
+  else
+    src = suffix + ((int64_t)k * (L - 1 - n_ctx) + (l - 1 - n_ctx)) * D;
+  f16x4 s = *(const f16x4*)(src + d);
+  f16x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = (f16)((float)s[e] + r16(pos[(int64_t)l * D + d + e]));
+  *(f16x4*)(x + row * D + d) = o;
+}
+
+// ---------------------------------------------------------------- deep prompt inject
+// x[n*L + row0 + r, :] = fp16(prompt[r, :])  (prompt fp32, the `.half()` at clip/model.py:327,344)
+__global__ void inject_kernel(f16* __restrict__ x, const float* __restrict__ prompt, int N, int L, int row0,
+                              int nrows, int D) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int total = N * nrows * D;
+  if (t >= total) return;
+  const int d = t % D;
+  const int r = (t / D) % nrows;
+  const int n = t / (D * nrows);
+  x[((int64_t)n * L + row0 + r) * D + d] = (f16)prompt[r * D + d];
+}
+
+// out[r, d] (=|+=) sum_n dx[n*L + row0 + r, d]  (fp32 accumulation, fixed n order), then the
+// injected rows of dx are zeroed (the previous layer's outputs there were discarded).
+// out_f16: round once to fp16 (fp16 source tensors, e.g. ctx / shared_ctx); else fp32.
+__global__ void inject_bwd_kernel(f16* __restrict__ dx, int N, int L, int row0, int nrows, int D, void* out,
+                                  int out_f16, int accumulate, int zero_rows) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nrows * D) return;
+  const int d = t % D, r = t / D;
+  float s = 0.f;
+  for (int n = 0; n < N; ++n) {
+    f16* p = dx + ((int64_t)n * L + row0 + r) * D + d;
+    s += (float)*p;
+    if (zero_rows) *p = (f16)0.f;
+  }
+  if (out_f16) {
+    f16* o = (f16*)out + t;
+    *o = accumulate ? (f16)((float)*o + r16(s)) : (f16)s;
+  } else {
+    float* o = (float*)out + t;
+    *o = accumulate ? *o + s : s;
+  }
+}
+
+// ---------------------------------------------------------------- transpose [R,C] -> [C,R]
+__global__ void transpose_kernel(const f16* __restrict__ in, int64_t ld_in, f16* __restrict__ out, int64_t ld_out,
+                                 int R, int C) {
+  __shared__ f16 tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: 64 x 4
+  for (int i = ty; i < 64; i += 4) {
+    const int r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? in[(int64_t)r * ld_in + c] : (f16)0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) out[(int64_t)c * ld_out + r] = tile[tx][i];
+  }
+}
+
+// ---------------------------------------------------------------- column sums (bias grads)
+constexpr int CS_ROWS = 256;
+__global__ void colsum_part_kernel(const f16* __restrict__ in, int64_t ld, int R, int C, float* __restrict__ part) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const int r0 = blockIdx.y * CS_ROWS;
+  const int r1 = min(R, r0 + CS_ROWS);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += (float)in[(int64_t)r * ld + c];
+  part[(int64_t)blockIdx.y * C + c] = s;
+}
+__global__ void colsum_final_kernel(const float* __restrict__ part, int nb, int C, void* out, int out_f16) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += part[(int64_t)b * C + c];
+  if (out_f16)
+    ((f16*)out)[c] = (f16)s;
+  else
+    ((float*)out)[c] = s;
+}
+
+// ---------------------------------------------------------------- small linears (M rows <= 16)
+// Y[m,o] = X[m,:] . W[o,:] + b[o]  (T = float: fp32 Linear, T = f16: fp16 Linear rounded once)
+template <typename T>
+__global__ void small_linear_fwd_kernel(const T* __restrict__ X, const T* __restrict__ W, const T* __restrict__ b,
+                                        T* __restrict__ Y, int M, int I, int O) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= M * O) return;
+  const int m = wave / O, o = wave % O;
+  float s = 0.f;
+  for (int i = lane; i < I; i += 64) s += (float)X[(int64_t)m * I + i] * (float)W[(int64_t)o * I + i];
+  s = wave_sum(s);
+  if (lane == 0) Y[(int64_t)m * O + o] = (T)(s + (b ? (float)b[o] : 0.f));
+}
+// dX[m,i] (=|+=) sum_o dY[m,o] W[o,i]   ; fp16 accumulate rounds the new term once then adds
+template <typename T>
+__global__ void small_linear_bwd_dx_kernel(const T* __restrict__ dY, const T* __restrict__ W, T* __restrict__ dX,
+                                           int M, int I, int O, int accumulate) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= M * I) return;
+  const int m = t / I, i = t % I;
+  float s = 0.f;
+  for (int o = 0; o < O; ++o) s += (float)dY[(int64_t)m * O + o] * (float)W[(int64_t)o * I + i];
+  if (accumulate)
+    dX[t] = (T)((float)dX[t] + (float)(T)s);
+  else
+    dX[t] = (T)s;
+}
+// dW[o,i] = sum_m dY[m,o] X[m,i] ; db[o] = sum_m dY[m,o]
+template <typename T>
+__global__ void small_linear_bwd_dw_kernel(const T* __restrict__ dY, const T* __restrict__ X, T* __restrict__ dW,
+                                           T* __restrict__ db, int M, int I, int O) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= O * I) return;
+  const int o = t / I, i = t % I;
+  float s = 0.f;
+  for (int m = 0; m < M; ++m) s += (float)dY[(int64_t)m * O + o] * (float)X[(int64_t)m * I + i];
+  dW[t] = (T)s;
+  if (i == 0 && db) {
+    float sb = 0.f;
+    for (int m = 0; m < M; ++m) sb += (float)dY[(int64_t)m * O + o];
+    db[o] = (T)sb;
+  }
+}
+
+// ---------------------------------------------------------------- casts
+__global__ void cast_f16_to_f32_kernel(const f16* __restrict__ in, float* __restrict__ out, int64_t n) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) out[t] = (float)in[t];
+}
+
+inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+
+}  // namespace
+
+extern "C" int mf_im2col_patch(const void* img, int img_is_f32, void* out, int B, int R, int P, void* stream) {
+  if (B <= 0) return 0;
+  if (R % P || (3 * P * P) % 8 || P % 8) return mf_set_error("mf_im2col_patch: bad geometry", -1);
+  const int G = R / P;
+  const int64_t total = (int64_t)B * G * G * (3 * P * P / 8);
+  hipStream_t st = (hipStream_t)stream;
+  if (img_is_f32)
+    im2col_kernel<float><<<nblk(total), 256, 0, st>>>((const float*)img, (f16*)out, B, R, P);
+  else
+    im2col_kernel<f16><<<nblk(total), 256, 0, st>>>((const f16*)img, (f16*)out, B, R, P);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_vision_assemble(const void* patch, const float* cls, const float* pos, const void* shared_ctx,
+                                  void* x, int B, int G2, int n_ctx, int D, void* stream) {
+  if (B <= 0) return 0;
+  if (D % 4) return mf_set_error("mf_vision_assemble: D % 4", -1);
+  const int64_t total = (int64_t)B * (G2 + 1 + n_ctx) * (D / 4);
+  vision_assemble_kernel<<<nblk(total), 256, 0, (hipStream_t)stream>>>(
+      (const f16*)patch, cls, pos, (const f16*)shared_ctx, (f16*)x, B, G2, n_ctx, D);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_text_assemble(const void* prefix, const void* ctx, const void* suffix, const float* pos, void* x,
+                                int K, int L, int n_ctx, int D, void* stream) {
+  if (K <= 0) return 0;
+  if (D % 4) return mf_set_error("mf_text_assemble: D % 4", -1);
+  const int64_t total = (int64_t)K * L * (D / 4);
+  text_assemble_kernel<<<nblk(total), 256, 0, (hipStream_t)stream>>>(
+      (const f16*)prefix, (const f16*)ctx, (const f16*)suffix, pos, (f16*)x, K, L, n_ctx, D);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_prompt_inject_fwd(void* x, const float* prompt, int N, int L, int row0, int nrows, int D,
+                                    void* stream) {
+  if (N <= 0) return 0;
+  if (row0 < 0 || row0 + nrows > L) return mf_set_error("mf_prompt_inject_fwd: rows out of range", -1);
+  inject_kernel<<<nblk((int64_t)N * nrows * D), 256, 0, (hipStream_t)stream>>>((f16*)x, prompt, N, L, row0, nrows, D);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_prompt_inject_bwd(void* dx, int N, int L, int row0, int nrows, int D, void* out, int out_f16,
+                                    int accumulate, int zero_rows, void* stream) {
+  if (row0 < 0 || row0 + nrows > L) return mf_set_error("mf_prompt_inject_bwd: rows out of range", -1);
+  inject_bwd_kernel<<<nblk((int64_t)nrows * D), 256, 0, (hipStream_t)stream>>>((f16*)dx, N, L, row0, nrows, D, out,
+                                                                               out_f16, accumulate, zero_rows);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_transpose_f16(const void* in, int64_t ld_in, void* out, int64_t ld_out, int R, int C,
+                                void* stream) {
+  if (R <= 0 || C <= 0) return 0;
+  dim3 grid((C + 63) / 64, (R + 63) / 64);
+  transpose_kernel<<<grid, 256, 0, (hipStream_t)stream>>>((const f16*)in, ld_in, (f16*)out, ld_out, R, C);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_colsum_blocks(int R) { return (R + CS_ROWS - 1) / CS_ROWS; }
+
+extern "C" int mf_colsum_f16(const void* in, int64_t ld, int R, int C, void* out, int out_f16, float* workspace,
+                             void* stream) {
+  if (R <= 0 || C <= 0) return 0;
+  const int nb = mf_colsum_blocks(R);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((C + 255) / 256, nb);
+  colsum_part_kernel<<<grid, 256, 0, st>>>((const f16*)in, ld, R, C, workspace);
+  MF_CHECK_LAUNCH();
+  colsum_final_kernel<<<(C + 255) / 256, 256, 0, st>>>(workspace, nb, C, out, out_f16);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_small_linear_fwd(const void* X, const void* W, const void* b, void* Y, int M, int I, int O,
+                                   int is_f16, void* stream) {
+  if (M <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t threads = (int64_t)M * O * 64;
+  if (is_f16)
+    small_linear_fwd_kernel<f16><<<nblk(threads), 256, 0, st>>>((const f16*)X, (const f16*)W, (const f16*)b, (f16*)Y,
+                                                               M, I, O);
+  else
+    small_linear_fwd_kernel<float><<<nblk(threads), 256, 0, st>>>((const float*)X, (const float*)W,
+                                                                  (const float*)b, (float*)Y, M, I, O);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_small_linear_bwd(const void* dY, const void* X, const void* W, void* dX, void* dW, void* db, int M,
+                                   int I, int O, int is_f16, int accumulate_dx, void* stream) {
+  if (M <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (is_f16) {
+    if (dX)
+      small_linear_bwd_dx_kernel<f16><<<nblk((int64_t)M * I), 256, 0, st>>>((const f16*)dY, (const f16*)W, (f16*)dX,
+                                                                            M, I, O, accumulate_dx);
+    if (dW)
+      small_linear_bwd_dw_kernel<f16><<<nblk((int64_t)O * I), 256, 0, st>>>((const f16*)dY, (const f16*)X, (f16*)dW,
+                                                                            (f16*)db, M, I, O);
+  } else {
+    if (dX)
+      small_linear_bwd_dx_kernel<float><<<nblk((int64_t)M * I), 256, 0, st>>>((const float*)dY, (const float*)W,
+                                                                              (float*)dX, M, I, O, accumulate_dx);
+    if (dW)
+      small_linear_bwd_dw_kernel<float><<<nblk((int64_t)O * I), 256, 0, st>>>((const float*)dY, (const float*)X,
+                                                                              (float*)dW, (float*)db, M, I, O);
+  }
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_cast_f16_f32(const void* in, float* out, int64_t n, void* stream) {
+  if (n <= 0) return 0;
+  cast_f16_to_f32_kernel<<<nblk(n), 256, 0, (hipStream_t)stream>>>((const f16*)in, out, n);
+  MF_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,232 @@
+// Cosine-logit head and MaPLe loss (trainers/maple.py:325,340-378):
+//   img_n = F.normalize(img, eps=1e-8), txt_n = F.normalize(txt, eps=1e-8)  (fp16: x / fp16(||x||))
+//   logits = fp16(min(exp(logit_scale),100) * fp16(img_n @ txt_n^T))
+//   loss   = CE(logits, y) + 0.5 * (1 - mean_b cos(img_n[b], txt_n[y_b]))
+// and the analytic backward to d img / d txt (fp32 math, fp16 outputs at the tensor boundaries
+// the reference materialises).  Small: B <= 64 rows, K <= 1000 classes, width 512.
+#include "mf_common.h"
+
+namespace {
+
+// one wave per row: y = fp16(x / fp16(norm)); norm16 saved
+__global__ void normalize_rows_kernel(const f16* __restrict__ x, f16* __restrict__ y, float* __restrict__ norm,
+                                      int rows, int D) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const f16* xr = x + (int64_t)row * D;
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    float v = (float)xr[d];
+    s += v * v;
+  }
+  s = wave_sum(s);
+  float n16 = r16(sqrtf(s));
+  n16 = fmaxf(n16, 1e-8f);
+  for (int d = lane; d < D; d += 64) y[(int64_t)row * D + d] = (f16)((float)xr[d] / n16);
+  if (lane == 0) norm[row] = n16;
+}
+
+// one wave per (b, k): mm = fp16(dot), logits = fp16(scale * mm)
+__global__ void logits_kernel(const f16* __restrict__ img_n, const f16* __restrict__ txt_n, int B, int K, int D,
+                              const float* __restrict__ logit_scale, f16* __restrict__ mm, f16* __restrict__ logits) {
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (w >= (int64_t)B * K) return;
+  const int b = w / K, k = w % K;
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) s += (float)img_n[(int64_t)b * D + d] * (float)txt_n[(int64_t)k * D + d];
+  s = wave_sum(s);
+  if (lane == 0) {
+    const float sc = fminf(expf(logit_scale[0]), 100.f);
+    const float m16 = r16(s);
+    mm[w] = (f16)m16;
+    logits[w] = (f16)(sc * m16);
+  }
+}
+
+// Single block of 256 threads (4 waves); wave w handles rows b = w, w+4, ...
+// out: loss_out[0] = total (fp16 value as fp32), [1] = CE, [2] = alignment, [3] = nonfinite flag
+// dmm[b,k] = fp16(fp16((softmax - onehot)/B) * scale);  cosg[b] = d cos[b] = fp16(-0.5/B)
+// cos needs u = fp16(img_n/||img_n||16), v = fp16(t/||t||16) (cosine_similarity normalises again)
+__global__ void loss_kernel(const f16* __restrict__ logits, const f16* __restrict__ img_n,
+                            const f16* __restrict__ txt_n, const int64_t* __restrict__ label, int B, int K, int D,
+                            const float* __restrict__ logit_scale, f16* __restrict__ dmm,
+                            float* __restrict__ cos_out, float* __restrict__ loss_out) {
+  __shared__ float s_ce[64], s_cos[64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const float sc = fminf(expf(logit_scale[0]), 100.f);
+  for (int b = w; b < B; b += 4) {
+    const f16* lr = logits + (int64_t)b * K;
+    const int y = (int)label[b];
+    float mx = -INFINITY;
+    for (int k = lane; k < K; k += 64) mx = fmaxf(mx, (float)lr[k]);
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int k = lane; k < K; k += 64) se += expf((float)lr[k] - mx);
+    se = wave_sum(se);
+    const float lse = logf(se);
+    const float logp_y = r16((float)lr[y] - mx - lse);  // log_softmax output is fp16
+    // d logits = fp16((softmax - onehot) / B), then * scale -> dmm (fp16)
+    for (int k = lane; k < K; k += 64) {
+      const float logp = r16((float)lr[k] - mx - lse);
+      const float g_nll = (k == y) ? r16(-1.0f / (float)B) : 0.f;
+      // log_softmax backward: g - exp(out) * sum(g)
+      const float dl = r16(g_nll - expf(logp) * r16(-1.0f / (float)B));
+      dmm[(int64_t)b * K + k] = (f16)(dl * sc);
+    }
+    // cosine similarity of img_n[b] and txt_n[y]
+    float su = 0.f, sv = 0.f;
+    for (int d = lane; d < D; d += 64) {
+      float a = (float)img_n[(int64_t)b * D + d], t = (float)txt_n[(int64_t)y * D + d];
+      su += a * a;
+      sv += t * t;
+    }
+    const float nu = fmaxf(r16(sqrtf(wave_sum(su))), 1e-8f), nv = fmaxf(r16(sqrtf(wave_sum(sv))), 1e-8f);
+    float c = 0.f;
+    for (int d = lane; d < D; d += 64) {
+      float a = r16((float)img_n[(int64_t)b * D + d] / nu), t = r16((float)txt_n[(int64_t)y * D + d] / nv);
+      c += r16(a * t);
+    }
+    c = r16(wave_sum(c));
+    if (lane == 0) {
+      s_ce[b] = -logp_y;
+      s_cos[b] = c;
+      cos_out[2 * b] = nu;
+      cos_out[2 * b + 1] = nv;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float ce = 0.f, cs = 0.f;
+    for (int b = 0; b < B; ++b) {
+      ce += s_ce[b];
+      cs += s_cos[b];
+    }
+    ce = r16(ce / (float)B);
+    const float align = r16(1.f - r16(cs / (float)B));
+    const float total = r16(ce + r16(0.5f * align));
+    loss_out[0] = total;
+    loss_out[1] = ce;
+    loss_out[2] = align;
+    loss_out[3] = isfinite(total) ? 0.f : 1.f;
+  }
+}
+
+// d img_n[b,:] = fp16( fp16(sum_k dmm[b,k] txt_n[k,:]) + cos-path ) ; block per row b
+// cos path (fp32): g_u = dcos*v, d img_n += g_u/nu - img_n*(g_u . img_n)/nu^3 with dcos = fp16(-0.5/B)
+__global__ void dimg_kernel(const f16* __restrict__ dmm, const f16* __restrict__ img_n, const f16* __restrict__ txt_n,
+                            const int64_t* __restrict__ label, const float* __restrict__ cos_norms, int B, int K,
+                            int D, f16* __restrict__ dimg_n) {
+  const int b = blockIdx.x;
+  const int y = (int)label[b];
+  const float dcos = r16(-0.5f / (float)B);
+  const float nu = cos_norms[2 * b], nv = cos_norms[2 * b + 1];
+  __shared__ float red[4];
+  // g_u . img_n
+  float dotp = 0.f;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float v = r16((float)txt_n[(int64_t)y * D + d] / nv);
+    dotp += dcos * v * (float)img_n[(int64_t)b * D + d];
+  }
+  dotp = wave_sum(dotp);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dotp;
+  __syncthreads();
+  dotp = red[0] + red[1] + red[2] + red[3];
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) s += (float)dmm[(int64_t)b * K + k] * (float)txt_n[(int64_t)k * D + d];
+    const float v = r16((float)txt_n[(int64_t)y * D + d] / nv);
+    const float a = (float)img_n[(int64_t)b * D + d];
+    const float cosg = dcos * v / nu - a * dotp / (nu * nu * nu);
+    dimg_n[(int64_t)b * D + d] = (f16)(r16(s) + r16(cosg));
+  }
+}
+
+// d txt_n[k,:] = fp16( fp16(sum_b dmm[b,k] img_n[b,:]) + sum_{b: y_b = k} cos-path ) ; block per k
+__global__ void dtxt_kernel(const f16* __restrict__ dmm, const f16* __restrict__ img_n, const f16* __restrict__ txt_n,
+                            const int64_t* __restrict__ label, const float* __restrict__ cos_norms, int B, int K,
+                            int D, f16* __restrict__ dtxt_n) {
+  const int k = blockIdx.x;
+  const float dcos = r16(-0.5f / (float)B);
+  __shared__ float red[4];
+  __shared__ float dots[64];
+  // per matching b: g_v . txt_n[k]
+  for (int b = 0; b < B; ++b) {
+    if ((int)label[b] != k) continue;  // uniform across the block
+    const float nu = cos_norms[2 * b];
+    float dotp = 0.f;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) {
+      float u = r16((float)img_n[(int64_t)b * D + d] / nu);
+      dotp += dcos * u * (float)txt_n[(int64_t)k * D + d];
+    }
+    dotp = wave_sum(dotp);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dotp;
+    __syncthreads();
+    if (threadIdx.x == 0) dots[b] = red[0] + red[1] + red[2] + red[3];
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += (float)dmm[(int64_t)b * K + k] * (float)img_n[(int64_t)b * D + d];
+    float cg = 0.f;
+    const float t = (float)txt_n[(int64_t)k * D + d];
+    for (int b = 0; b < B; ++b) {
+      if ((int)label[b] != k) continue;
+      const float nu = cos_norms[2 * b], nv = cos_norms[2 * b + 1];
+      const float u = r16((float)img_n[(int64_t)b * D + d] / nu);
+      cg += dcos * u / nv - t * dots[b] / (nv * nv * nv);
+    }
+    dtxt_n[(int64_t)k * D + d] = (f16)(r16(s) + (cg != 0.f ? r16(cg) : 0.f));
+  }
+}
+
+// normalize backward: dx = fp16(dy/n - x * (dy . x) / n^3)   ; one wave per row
+__global__ void normalize_bwd_kernel(const f16* __restrict__ x, const f16* __restrict__ dy,
+                                     const float* __restrict__ norm, f16* __restrict__ dx, int rows, int D) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float n = norm[row];
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) s += (float)dy[(int64_t)row * D + d] * (float)x[(int64_t)row * D + d];
+  s = wave_sum(s);
+  for (int d = lane; d < D; d += 64) {
+    const float g = (float)dy[(int64_t)row * D + d] / n - (float)x[(int64_t)row * D + d] * s / (n * n * n);
+    dx[(int64_t)row * D + d] = (f16)g;
+  }
+}
+
+}  // namespace
+
+// workspace floats needed: 2*B (cos norms) + (B+K) (feature norms)
+extern "C" int mf_clip_head_fwd(const void* img, const void* txt, int B, int K, int D, const float* logit_scale,
+                                void* img_n, void* txt_n, float* norms, void* mm, void* logits, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  normalize_rows_kernel<<<(B + 3) / 4, 256, 0, st>>>((const f16*)img, (f16*)img_n, norms, B, D);
+  normalize_rows_kernel<<<(K + 3) / 4, 256, 0, st>>>((const f16*)txt, (f16*)txt_n, norms + B, K, D);
+  const int64_t threads = (int64_t)B * K * 64;
+  logits_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, st>>>((const f16*)img_n, (const f16*)txt_n, B, K, D,
+                                                                   logit_scale, (f16*)mm, (f16*)logits);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_clip_loss_fwd_bwd(const void* img, const void* txt, const void* img_n, const void* txt_n,
+                                    const float* norms, const void* logits, const int64_t* label, int B, int K, int D,
+                                    const float* logit_scale, void* dmm, float* cos_ws, float* loss_out,
+                                    void* dimg_n, void* dtxt_n, void* dimg, void* dtxt, void* stream) {
+  if (B > 64) return mf_set_error("mf_clip_loss_fwd_bwd: B <= 64", -1);
+  hipStream_t st = (hipStream_t)stream;
+  loss_kernel<<<1, 256, 0, st>>>((const f16*)logits, (const f16*)img_n, (const f16*)txt_n, label, B, K, D,
+                                 logit_scale, (f16*)dmm, cos_ws, loss_out);
+  dimg_kernel<<<B, 256, 0, st>>>((const f16*)dmm, (const f16*)img_n, (const f16*)txt_n, label, cos_ws, B, K, D,
+                                 (f16*)dimg_n);
+  dtxt_kernel<<<K, 256, 0, st>>>((const f16*)dmm, (const f16*)img_n, (const f16*)txt_n, label, cos_ws, B, K, D,
+                                 (f16*)dtxt_n);
+  normalize_bwd_kernel<<<(B + 3) / 4, 256, 0, st>>>((const f16*)img, (const f16*)dimg_n, norms, (f16*)dimg, B, D);
+  normalize_bwd_kernel<<<(K + 3) / 4, 256, 0, st>>>((const f16*)txt, (const f16*)dtxt_n, norms + B, (f16*)dtxt, K, D);
+  MF_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,222 @@
+// LayerNorm forward/backward for CLIP's fp16 LayerNorm subclass (clip/model.py:153-159):
+// fp16 rows in, statistics and affine math in fp32, fp16 out; gamma/beta are fp32 and trainable
+// everywhere (trainers/maple.py:451-454), so the backward also produces dgamma/dbeta.
+//
+// HBM-bound: 2 B read + 2 B write per element forward, ~6 B per element backward.  One wave per
+// row, 8-byte (4 x fp16) vector accesses, statistics by wave64 shuffles.  An optional int32 row
+// index gathers rows (ln_post on each image's class token, ln_final on each prompt's EOT token,
+// clip/model.py:567 and trainers/maple.py:72-76).  dgamma/dbeta are reduced deterministically:
+// per-block partial sums, then a column reduction (no float atomics).
+#include "mf_common.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int LN_WAVES = 4;
+constexpr int LN_ROWS_PER_BLOCK = 32;
+
+// y = ((x*rstd) + (-rstd*mean)) * gamma + beta, the operation order of torch's CPU kernel
+template <int D>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const f16* __restrict__ x, int64_t ldx,
+                                                    const int* __restrict__ ridx, const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta, f16* __restrict__ y,
+                                                    int64_t ldy, float* __restrict__ mean_out,
+                                                    float* __restrict__ rstd_out, int rows) {
+  constexpr int CH = D / 256;  // vec4 chunks per lane
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int src = ridx ? ridx[row] : row;
+  const f16* xr = x + (int64_t)src * ldx;
+  float v[CH * 4];
+  float s = 0.f;
+#pragma unroll
+  for (int cnt = 0; cnt < CH; ++cnt) {
+    const int c = lane + 64 * cnt;
+    f16x4 t = *(const f16x4*)(xr + 4 * c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[cnt * 4 + e] = (float)t[e];
+      s += v[cnt * 4 + e];
+    }
+  }
+  const float mean = wave_sum(s) / (float)D;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < CH * 4; ++i) {
+    float d = v[i] - mean;
+    ss += d * d;
+  }
+  const float var = wave_sum(ss) / (float)D;
+  const float rstd = 1.0f / sqrtf(fmaxf(var, 0.f) + 1e-5f);
+  const float bias = -rstd * mean;
+  f16* yr = y + (int64_t)row * ldy;
+#pragma unroll
+  for (int cnt = 0; cnt < CH; ++cnt) {
+    const int c = lane + 64 * cnt;
+    f32x4 g = *(const f32x4*)(gamma + 4 * c);
+    f32x4 b = *(const f32x4*)(beta + 4 * c);
+    f16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = v[cnt * 4 + e] * rstd;
+      t = t + bias;
+      t = t * g[e];
+      t = t + b[e];
+      o[e] = (f16)t;
+    }
+    *(f16x4*)(yr + 4 * c) = o;
+  }
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
+// dx = rstd*(dy*g) + b*x + c with  b = (sum(dy*g)*mean - sum(dy*g*x)) * rstd^3 / D,
+// c = -b*mean - sum(dy*g)*rstd/D   (fp32), then dx16 = fp16(dx) and, when a residual gradient
+// is given, out = fp16(dres + dx16)  (the autograd accumulation of the two uses of x).
+template <int D>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const f16* __restrict__ dy, int64_t lddy,
+                                                    const f16* __restrict__ x, int64_t ldx,
+                                                    const int* __restrict__ ridx, const float* __restrict__ gamma,
+                                                    const float* __restrict__ mean_in,
+                                                    const float* __restrict__ rstd_in, const f16* dres,
+                                                    int64_t ldres, f16* dx, int64_t lddx,
+                                                    float* __restrict__ dg_part, float* __restrict__ db_part,
+                                                    int rows) {
+  constexpr int CH = D / 256;
+  __shared__ float red_g[LN_WAVES][D];
+  __shared__ float red_b[LN_WAVES][D];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  float accg[CH * 4], accb[CH * 4];
+#pragma unroll
+  for (int i = 0; i < CH * 4; ++i) accg[i] = accb[i] = 0.f;
+  const int r0 = blockIdx.x * LN_ROWS_PER_BLOCK;
+  for (int rr = w; rr < LN_ROWS_PER_BLOCK; rr += LN_WAVES) {
+    const int row = r0 + rr;
+    if (row >= rows) break;
+    const int src = ridx ? ridx[row] : row;
+    const f16* xr = x + (int64_t)src * ldx;
+    const f16* dyr = dy + (int64_t)row * lddy;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xv[CH * 4], dv[CH * 4], gv[CH * 4];
+    float sdg = 0.f, sdgx = 0.f;
+#pragma unroll
+    for (int cnt = 0; cnt < CH; ++cnt) {
+      const int c = lane + 64 * cnt;
+      f16x4 tx = *(const f16x4*)(xr + 4 * c);
+      f16x4 td = *(const f16x4*)(dyr + 4 * c);
+      f32x4 g = *(const f32x4*)(gamma + 4 * c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xv[cnt * 4 + e] = (float)tx[e];
+        dv[cnt * 4 + e] = (float)td[e];
+        gv[cnt * 4 + e] = g[e];
+        float dg = dv[cnt * 4 + e] * g[e];
+        sdg += dg;
+        sdgx += dg * xv[cnt * 4 + e];
+        float xhat = (xv[cnt * 4 + e] - mean) * rstd;
+        accg[cnt * 4 + e] += dv[cnt * 4 + e] * xhat;
+        accb[cnt * 4 + e] += dv[cnt * 4 + e];
+      }
+    }
+    sdg = wave_sum(sdg);
+    sdgx = wave_sum(sdgx);
+    const float invD = 1.0f / (float)D;
+    const float b = (sdg * mean - sdgx) * rstd * rstd * rstd * invD;
+    const float c = -b * mean - sdg * rstd * invD;
+    f16* dxr = dx + (int64_t)src * lddx;
+    const f16* drr = dres ? dres + (int64_t)src * ldres : nullptr;
+#pragma unroll
+    for (int cnt = 0; cnt < CH; ++cnt) {
+      const int cc = lane + 64 * cnt;
+      f16x4 o;
+      f16x4 rv;
+      if (drr) rv = *(const f16x4*)(drr + 4 * cc);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = ((rstd * dv[cnt * 4 + e]) * gv[cnt * 4 + e] + b * xv[cnt * 4 + e]) + c;
+        float t16 = r16(t);
+        o[e] = drr ? (f16)((float)rv[e] + t16) : (f16)t16;
+      }
+      *(f16x4*)(dxr + 4 * cc) = o;
+    }
+  }
+  // reduce the 4 waves' column partials through LDS
+#pragma unroll
+  for (int cnt = 0; cnt < CH; ++cnt) {
+    const int c = lane + 64 * cnt;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red_g[w][4 * c + e] = accg[cnt * 4 + e];
+      red_b[w][4 * c + e] = accb[cnt * 4 + e];
+    }
+  }
+  __syncthreads();
+  for (int col = threadIdx.x; col < D; col += 256) {
+    float sg = 0.f, sb = 0.f;
+#pragma unroll
+    for (int k = 0; k < LN_WAVES; ++k) {
+      sg += red_g[k][col];
+      sb += red_b[k][col];
+    }
+    dg_part[(int64_t)blockIdx.x * D + col] = sg;
+    db_part[(int64_t)blockIdx.x * D + col] = sb;
+  }
+}
+
+// out[col] (=|+=) sum_b part[b][col], fixed order -> deterministic
+__global__ void col_reduce_f32_kernel(const float* __restrict__ part, int nblk, int D, float* __restrict__ out,
+                                      int accumulate) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= D) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * D + col];
+  out[col] = accumulate ? out[col] + s : s;
+}
+
+}  // namespace
+
+extern "C" int mf_layernorm_fwd(const void* x, int64_t ldx, const int* row_index, const float* gamma,
+                                const float* beta, void* y, int64_t ldy, float* mean, float* rstd, int rows, int D,
+                                void* stream) {
+  if (rows <= 0) return 0;
+  dim3 grid((rows + LN_WAVES - 1) / LN_WAVES);
+  hipStream_t st = (hipStream_t)stream;
+  if (D == 768)
+    ln_fwd_kernel<768><<<grid, 256, 0, st>>>((const f16*)x, ldx, row_index, gamma, beta, (f16*)y, ldy, mean, rstd, rows);
+  else if (D == 512)
+    ln_fwd_kernel<512><<<grid, 256, 0, st>>>((const f16*)x, ldx, row_index, gamma, beta, (f16*)y, ldy, mean, rstd, rows);
+  else
+    return mf_set_error("mf_layernorm_fwd: D must be 512 or 768", -1);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_layernorm_bwd_blocks(int rows) { return (rows + LN_ROWS_PER_BLOCK - 1) / LN_ROWS_PER_BLOCK; }
+
+extern "C" int mf_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const int* row_index,
+                                const float* gamma, const float* mean, const float* rstd, const void* dres,
+                                int64_t ldres, void* dx, int64_t lddx, float* dgamma, float* dbeta, float* workspace,
+                                int rows, int D, int accumulate, void* stream) {
+  if (rows <= 0) return 0;
+  if (D != 512 && D != 768) return mf_set_error("mf_layernorm_bwd: D must be 512 or 768", -1);
+  const int nblk = mf_layernorm_bwd_blocks(rows);
+  float* dg_part = workspace;
+  float* db_part = workspace + (int64_t)nblk * D;
+  hipStream_t st = (hipStream_t)stream;
+  if (D == 768)
+    ln_bwd_kernel<768><<<nblk, 256, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, row_index, gamma, mean, rstd,
+                                             (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows);
+  else
+    ln_bwd_kernel<512><<<nblk, 256, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, row_index, gamma, mean, rstd,
+                                             (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows);
+  MF_CHECK_LAUNCH();
+  col_reduce_f32_kernel<<<(D + 255) / 256, 256, 0, st>>>(dg_part, nblk, D, dgamma, accumulate);
+  col_reduce_f32_kernel<<<(D + 255) / 256, 256, 0, st>>>(db_part, nblk, D, dbeta, accumulate);
+  MF_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,61 @@
+// Shared helpers for the MI355X (gfx950 / CDNA4) kernels of the federated MaPLe path.
+// Everything here is device-side plumbing: vector types for MFMA fragments, fp16 rounding
+// helpers that pin the reference's rounding points, wave64 reductions and the C-ABI status
+// convention (int status, mf_last_error()).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef _Float16 f16;
+typedef f16 f16x2 __attribute__((ext_vector_type(2)));
+typedef f16 f16x4 __attribute__((ext_vector_type(4)));
+typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+#define MF_DEV __device__ __forceinline__
+
+// Round-to-nearest-even fp32 -> fp16 -> fp32: the rounding every fp16 torch op applies once
+// to its opmath (fp32) result.
+MF_DEV float r16(float x) { return (float)(f16)x; }
+
+MF_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+MF_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// QuickGELU with the reference's three fp16 roundings (clip/model.py:162-164):
+//   t1 = fp16(1.702*f); t2 = fp16(sigmoid(t1)); g = fp16(f*t2)
+MF_DEV float quick_gelu16(float f, float* t2_out) {
+  float t1 = r16(f * 1.702f);
+  float t2 = r16(1.0f / (1.0f + __expf(-t1)));
+  *t2_out = t2;
+  return r16(f * t2);
+}
+// Its autograd backward (mul / sigmoid / mul nodes, then fp16 accumulation of the two uses of f):
+//   da = fp16(dg*t2); dt2 = fp16(dg*f); db = fp16(dt1*1.702); df = fp16(da+db), where torch's CPU
+//   sigmoid_backward for Half runs in fp16 arithmetic op by op (measured against
+//   aten::sigmoid_backward): dt1 = fp16(fp16(dt2*fp16(1-t2))*t2)
+MF_DEV float quick_gelu16_bwd(float dg, float f) {
+  float t1 = r16(f * 1.702f);
+  float t2 = r16(1.0f / (1.0f + __expf(-t1)));
+  float da = r16(dg * t2);
+  float dt2 = r16(dg * f);
+  float dt1 = r16(r16(dt2 * r16(1.0f - t2)) * t2);
+  float db = r16(dt1 * 1.702f);
+  return r16(da + db);
+}
+
+#define MF_CHECK_LAUNCH()                                                     \
+  do {                                                                        \
+    hipError_t _e = hipGetLastError();                                        \
+    if (_e != hipSuccess) return mf_set_error(hipGetErrorString(_e), (int)_e); \
+  } while (0)
+
+extern "C" int mf_set_error(const char* msg, int code);

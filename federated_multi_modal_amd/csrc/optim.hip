@@ -1,0 +1,196 @@
+// Optimizer step and federated averaging over the flat trainable buffers.
+//
+// The trainable tensors (trainers/maple.py:447-479) live in two flat device buffers, one fp16 and
+// one fp32, each tensor a contiguous segment; grads and SGD momentum mirror them.  That turns
+//   torch.nn.utils.clip_grad_norm_(params, 1.0)      (trainers/maple.py:592-596)
+//   Dassl SGD(momentum 0.9, wd 5e-4).step()           (trainers/maple.py:598)
+//   safe_average_weights / check_weights_valid        (trainers/maple_fed.py:309-325)
+// into a handful of streaming kernels with no host synchronisation: the clip coefficient stays on
+// the device and the SGD kernel reads it.
+//
+// Rounding points follow torch: per-tensor norms in the grad's dtype (fp16 norm for fp16 grads),
+// total norm in fp32, coef = clamp(1/(total+1e-6), max 1); g = T(g*coef); d_p = T(g + wd*p);
+// buf = d_p (first step) or T(T(buf*mom) + d_p); p = T(p - lr*buf).
+#include "mf_common.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int CHUNK = 8192;
+
+struct Chunk {
+  int seg;
+  int is16;
+  int64_t start, end;  // element range inside the segment's flat buffer
+};
+
+__global__ void sumsq_chunks_kernel(const f16* __restrict__ g16, const float* __restrict__ g32,
+                                    const Chunk* __restrict__ chunks, float* __restrict__ part) {
+  const Chunk c = chunks[blockIdx.x];
+  float s = 0.f;
+  if (c.is16) {
+    for (int64_t i = c.start + threadIdx.x; i < c.end; i += blockDim.x) {
+      float v = (float)g16[i];
+      s += v * v;
+    }
+  } else {
+    for (int64_t i = c.start + threadIdx.x; i < c.end; i += blockDim.x) {
+      float v = g32[i];
+      s += v * v;
+    }
+  }
+  __shared__ float red[4];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// One block: per-segment norms (chunks of a segment are consecutive), total, clip coefficient.
+// out[0] = total norm, out[1] = clip coef, out[2] = 1 if total is finite else 0
+__global__ void clip_coef_kernel(const float* __restrict__ part, const Chunk* __restrict__ chunks, int nchunks,
+                                 float max_norm, float* __restrict__ out) {
+  __shared__ float red[256];
+  float acc = 0.f;
+  // every thread walks the chunk list; thread t owns the segments whose index % 256 == t
+  int c = 0;
+  while (c < nchunks) {
+    const int seg = chunks[c].seg;
+    const int is16 = chunks[c].is16;
+    float ss = 0.f;
+    int cc = c;
+    while (cc < nchunks && chunks[cc].seg == seg) ss += part[cc++];
+    if ((seg & 255) == (int)threadIdx.x) {
+      float nrm = sqrtf(ss);
+      if (is16) nrm = r16(nrm);
+      acc += nrm * nrm;
+    }
+    c = cc;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int i = 0; i < 256; ++i) tot += red[i];
+    const float total = sqrtf(tot);
+    float coef = max_norm / (total + 1e-6f);
+    coef = coef > 1.f ? 1.f : coef;
+    out[0] = total;
+    out[1] = coef;
+    out[2] = isfinite(total) ? 1.f : 0.f;
+  }
+}
+
+// hyper = {lr, momentum, weight_decay, first_step (1.0 = momentum buffer not yet created)}: read from
+// device memory so a captured step replays with the current schedule value.
+template <typename T>
+__global__ void sgd_kernel(T* __restrict__ p, T* __restrict__ g, T* __restrict__ buf, int64_t n,
+                           const float* __restrict__ coef_ptr, const float* __restrict__ hyper) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float coef = coef_ptr[1];
+  const float lr = hyper[0], momentum = hyper[1], wd = hyper[2];
+  const bool first = hyper[3] != 0.f;
+  const float pv = (float)p[i];
+  const float gc = (float)(T)((float)g[i] * coef);
+  g[i] = (T)gc;
+  const float dp = (float)(T)(gc + wd * pv);
+  float b;
+  if (first)
+    b = dp;
+  else
+    b = (float)(T)((float)(T)((float)buf[i] * momentum) + dp);
+  buf[i] = (T)b;
+  p[i] = (T)(pv + (-lr) * b);
+}
+
+// bucket[0:n16] = float(p16), bucket[n16:n16+n32] = p32
+__global__ void pack_kernel(const f16* __restrict__ p16, int64_t n16, const float* __restrict__ p32, int64_t n32,
+                            float* __restrict__ bucket) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n16)
+    bucket[i] = (float)p16[i];
+  else if (i < n16 + n32)
+    bucket[i] = p32[i - n16];
+}
+
+// mean = sum / n ; value = fp16(mean) ; p16 = value, p32 = float(value)   (the `.half()` of
+// trainers/maple_fed.py:314 followed by load_state_dict into each parameter's dtype)
+__global__ void unpack_kernel(const float* __restrict__ bucket, float n_valid, f16* __restrict__ p16, int64_t n16,
+                              float* __restrict__ p32, int64_t n32) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n16) {
+    p16[i] = (f16)(bucket[i] / n_valid);
+  } else if (i < n16 + n32) {
+    p32[i - n16] = r16(bucket[i] / n_valid);
+  }
+}
+
+// flag[0] |= 1 if any element is NaN/Inf
+__global__ void nonfinite_kernel(const void* __restrict__ x, int64_t n, int is16, int* __restrict__ flag) {
+  int bad = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = is16 ? (float)((const f16*)x)[i] : ((const float*)x)[i];
+    bad |= !isfinite(v);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+
+}  // namespace
+
+extern "C" int mf_optim_chunk_bytes() { return (int)sizeof(Chunk); }
+extern "C" int mf_optim_chunk_elems() { return CHUNK; }
+
+// chunks: device array of Chunk {int seg, int is16, int64 start, int64 end}; part: nchunks floats;
+// out: 3 floats (total norm, coef, finite flag)
+extern "C" int mf_clip_grad_norm(const void* g16, const float* g32, const void* chunks, int nchunks, float max_norm,
+                                 float* part, float* out, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (nchunks <= 0) return 0;
+  sumsq_chunks_kernel<<<nchunks, 256, 0, st>>>((const f16*)g16, g32, (const Chunk*)chunks, part);
+  MF_CHECK_LAUNCH();
+  clip_coef_kernel<<<1, 256, 0, st>>>(part, (const Chunk*)chunks, nchunks, max_norm, out);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_sgd_step(void* p, void* g, void* buf, int64_t n, int is16, const float* coef,
+                           const float* hyper, void* stream) {
+  if (n <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (is16)
+    sgd_kernel<f16><<<nblk(n), 256, 0, st>>>((f16*)p, (f16*)g, (f16*)buf, n, coef, hyper);
+  else
+    sgd_kernel<float><<<nblk(n), 256, 0, st>>>((float*)p, (float*)g, (float*)buf, n, coef, hyper);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_fedavg_pack(const void* p16, int64_t n16, const float* p32, int64_t n32, float* bucket,
+                              void* stream) {
+  if (n16 + n32 <= 0) return 0;
+  pack_kernel<<<nblk(n16 + n32), 256, 0, (hipStream_t)stream>>>((const f16*)p16, n16, p32, n32, bucket);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_fedavg_unpack(const float* bucket, float n_valid, void* p16, int64_t n16, float* p32, int64_t n32,
+                                void* stream) {
+  if (n16 + n32 <= 0) return 0;
+  if (!(n_valid >= 1.f)) return mf_set_error("mf_fedavg_unpack: n_valid must be >= 1", -1);
+  unpack_kernel<<<nblk(n16 + n32), 256, 0, (hipStream_t)stream>>>(bucket, n_valid, (f16*)p16, n16, p32, n32);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_nonfinite_flag(const void* x, int64_t n, int is16, int* flag, void* stream) {
+  if (n <= 0) return 0;
+  unsigned g = nblk(n);
+  if (g > 2048) g = 2048;
+  nonfinite_kernel<<<g, 256, 0, (hipStream_t)stream>>>(x, n, is16, flag);
+  MF_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,557 @@
+"""MaPLe client engine: explicit forward + backward + optimizer step of one federated client on one
+MI355X, every op a libmapfed.so kernel over preallocated HBM buffers.
+
+What it computes is CustomCLIP.forward + loss.backward + clip_grad_norm_ + SGD.step of the reference
+(trainers/maple.py:304-381, 586-598) for the MaPLe towers of clip/model.py:269-572, with the freeze
+policy of trainers/maple.py:447-479.  Because the graph is static, the backward is written out by
+hand instead of recorded by autograd:
+
+* dX flows through all 12 blocks of both towers (LN params and prompts are trainable everywhere);
+* weight gradients are produced only for block 11 of each tower, every LayerNorm, and the prompt
+  learner (nothing else is trainable);
+* injected prompt rows are reduced over the batch into the prompt gradient and zeroed in dX, which
+  is exactly autograd's result for the `torch.cat([prefix, prompt])` replacement.
+
+Data layout in HBM: activations are [N*L, D] row-major, batch-major (row n*L + l);
+the reference's LND permutes are layout-only and vanish.  Per layer the forward saves exactly what
+its backward reads (X, QKV, O, LSE, X1, pre-GELU F, LN statistics); block 11 also keeps the LN
+outputs and GELU output for its weight gradients.  Trainable parameters live in two flat buffers
+(fp16 / fp32) with matching gradient and momentum buffers, so clip-norm, SGD and FedAvg are single
+streaming kernels and FedAvg is one RCCL all-reduce of one contiguous bucket.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import ops
+from . import synthetic as syn
+
+F16, F32 = torch.float16, torch.float32
+N_CTX = 2
+
+
+@dataclass
+class EngineConfig:
+    batch: int                  # B images per client step
+    classnames: List[str]       # K classes (text prompts)
+    prompt_depth: int = 9       # J (cfg.TRAINER.MAPLE.PROMPT_DEPTH, train.py:113)
+    seed: int = 0
+    n_ctx: int = N_CTX
+    ctx_init: str = "a photo of a"
+    dims: syn.ClipDims = field(default_factory=syn.ClipDims)
+    momentum: float = 0.9       # Dassl SGD defaults (cfg.OPTIM.MOMENTUM / WEIGHT_DECAY)
+    weight_decay: float = 5e-4
+    max_grad_norm: float = 1.0
+
+
+def _is_trainable(name: str) -> bool:
+    """trainers/maple.py:447-479."""
+    if name.startswith("prompt_learner.") and not name.startswith("prompt_learner.token_"):
+        return True
+    if "ln_" in name:
+        return True
+    return "transformer.resblocks.11." in name
+
+
+_FP16_SUFFIX = ("conv1.weight", "in_proj_weight", "in_proj_bias", "out_proj.weight", "out_proj.bias",
+                "c_fc.weight", "c_fc.bias", "c_proj.weight", "c_proj.bias")
+
+
+def reference_param_specs(cfg: EngineConfig) -> List[Tuple[str, Tuple[int, ...], torch.dtype]]:
+    """(name, shape, dtype) of every CustomCLIP parameter the path uses, in named_parameters order."""
+    d = cfg.dims
+    dv, dt = d.vision_width, d.text_width
+    specs: List[Tuple[str, Tuple[int, ...], torch.dtype]] = []
+    pl = "prompt_learner."
+    specs += [(pl + "ctx", (cfg.n_ctx, dt), F16),
+              (pl + "proj_lang_to_vis.weight", (dv, dt), F16), (pl + "proj_lang_to_vis.bias", (dv,), F16),
+              (pl + "proj_vis_to_lang.weight", (dt, dv), F16), (pl + "proj_vis_to_lang.bias", (dt,), F16)]
+    J = cfg.prompt_depth
+    for k in range((J - 1 + 1) // 2):
+        specs.append((pl + f"compound_prompts_text_parameters.{k}", (cfg.n_ctx, dt), F32))
+    for k in range((J - 1) // 2):
+        specs.append((pl + f"visual_deep_prompts_parameters.{k}", (cfg.n_ctx, dv), F32))
+    for i in range(J - 1):
+        fin, fout = (dt, dv) if i % 2 == 0 else (dv, dt)
+        specs += [(pl + f"compound_prompt_projections.{i}.weight", (fout, fin), F32),
+                  (pl + f"compound_prompt_projections.{i}.bias", (fout,), F32)]
+    ie = "image_encoder."
+    g = d.grid
+    specs += [(ie + "class_embedding", (dv,), F32), (ie + "positional_embedding", (g * g + 1, dv), F32),
+              (ie + "proj", (dv, d.embed_dim), F16), (ie + "conv1.weight", (dv, 3, d.vision_patch, d.vision_patch), F16),
+              (ie + "ln_pre.weight", (dv,), F32), (ie + "ln_pre.bias", (dv,), F32)]
+
+    def blocks(prefix, D, n):
+        out = []
+        for i in range(n):
+            p = f"{prefix}.resblocks.{i}."
+            out += [(p + "attn.in_proj_weight", (3 * D, D), F16), (p + "attn.in_proj_bias", (3 * D,), F16),
+                    (p + "attn.out_proj.weight", (D, D), F16), (p + "attn.out_proj.bias", (D,), F16),
+                    (p + "ln_1.weight", (D,), F32), (p + "ln_1.bias", (D,), F32),
+                    (p + "mlp.c_fc.weight", (4 * D, D), F16), (p + "mlp.c_fc.bias", (4 * D,), F16),
+                    (p + "mlp.c_proj.weight", (D, 4 * D), F16), (p + "mlp.c_proj.bias", (D,), F16),
+                    (p + "ln_2.weight", (D,), F32), (p + "ln_2.bias", (D,), F32)]
+        return out
+
+    specs += blocks(ie + "transformer", dv, d.vision_layers)
+    specs += [(ie + "ln_post.weight", (dv,), F32), (ie + "ln_post.bias", (dv,), F32)]
+    te = "text_encoder."
+    specs += blocks(te + "transformer", dt, d.text_layers)
+    specs += [(te + "positional_embedding", (d.context_length, dt), F32), (te + "ln_final.weight", (dt,), F32),
+              (te + "ln_final.bias", (dt,), F32), (te + "text_projection", (dt, d.embed_dim), F16),
+              ("logit_scale", (), F32)]
+    return specs
+
+
+def synthetic_state(cfg: EngineConfig) -> Dict[str, np.ndarray]:
+    """Synthetic values for every spec, keyed by CustomCLIP parameter name (numpy fp32)."""
+    d = cfg.dims
+    sd = syn.clip_state_dict(cfg.seed, d, vision_layers=d.vision_layers, text_layers=d.text_layers)
+    out: Dict[str, np.ndarray] = {}
+    for k, v in sd.items():
+        if k == "logit_scale":
+            continue
+        if k.startswith("visual."):
+            out["image_encoder." + k[7:]] = v
+        elif k in ("positional_embedding", "ln_final.weight", "ln_final.bias", "text_projection") or \
+                k.startswith("transformer."):
+            out["text_encoder." + k] = v
+    init = syn.tokenize(cfg.ctx_init)
+    out["prompt_learner.ctx"] = syn.token_embedding_rows(cfg.seed, init[0, 1:1 + cfg.n_ctx])
+    for k, v in syn.prompt_learner_params(cfg.seed, cfg.prompt_depth, cfg.n_ctx).items():
+        out["prompt_learner." + k] = v
+    out["logit_scale"] = np.array(math.log(1 / 0.07), dtype=np.float32)
+    return out
+
+
+class _Tower:
+    """Buffers + forward/backward schedule of one 12-block transformer tower."""
+
+    def __init__(self, eng: "MapleEngine", name: str, N: int, L: int, D: int, H: int, layers: int,
+                 causal: bool, inject_row0: int):
+        self.e, self.name, self.N, self.L, self.D, self.H = eng, name, N, L, D, H
+        self.layers, self.causal, self.row0 = layers, causal, inject_row0
+        dev = eng.device
+        R = N * L
+        self.R = R
+        self.Rp = ((R + 63) // 64) * 64  # padded row count (K dim of the dW GEMMs)
+        e = lambda *s, dt=F16: torch.empty(*s, device=dev, dtype=dt)
+        self.X = [e(R, D) for _ in range(layers + 1)]
+        self.QKV = [e(R, 3 * D) for _ in range(layers)]
+        self.O = [e(R, D) for _ in range(layers)]
+        self.X1 = [e(R, D) for _ in range(layers)]
+        self.Fp = [e(R, 4 * D) for _ in range(layers)]
+        self.LSE = [e(N * H * L, dt=F32) for _ in range(layers)]
+        self.mean1 = [e(R, dt=F32) for _ in range(layers)]
+        self.rstd1 = [e(R, dt=F32) for _ in range(layers)]
+        self.mean2 = [e(R, dt=F32) for _ in range(layers)]
+        self.rstd2 = [e(R, dt=F32) for _ in range(layers)]
+        self.H1 = e(R, D)
+        self.H2 = e(R, D)
+        self.G = e(R, 4 * D)
+        # backward
+        self.dX = e(R, D)
+        self.dX1 = e(R, D)
+        self.dO = e(R, D)
+        self.dH = e(R, D)
+        self.dQKV = e(R, 3 * D)
+        self.dF = e(R, 4 * D)
+        self.attn_ws = e(N * H * L, dt=F32)
+        self.ln_ws = e(ops.layernorm_ws_floats(R, D), dt=F32)
+        self.cs_ws = e(ops.colsum_ws_floats(R, 4 * D), dt=F32)
+        # transposed operands of the block-11 weight gradients (zero padded to Rp columns)
+        self.tA = torch.zeros(4 * D, self.Rp, device=dev, dtype=F16)
+        self.tB = torch.zeros(4 * D, self.Rp, device=dev, dtype=F16)
+
+    # -- parameters of block i
+    def p(self, i: int, key: str) -> torch.Tensor:
+        return self.e.P[f"{self.name}.transformer.resblocks.{i}.{key}"]
+
+    def wt(self, i: int, key: str) -> torch.Tensor:
+        return self.e.WT[f"{self.name}.transformer.resblocks.{i}.{key}"]
+
+    def g(self, i: int, key: str) -> torch.Tensor:
+        return self.e.G[f"{self.name}.transformer.resblocks.{i}.{key}"]
+
+    # ------------------------------------------------------------------------------------------
+    def forward(self, deep_prompts: List[torch.Tensor]):
+        """X[0] must be filled.  deep_prompts[j] (fp32 [n_ctx, D]) is injected before layer j+1."""
+        N, L, D, H = self.N, self.L, self.D, self.H
+        for i in range(self.layers):
+            x = self.X[i]
+            if 1 <= i <= len(deep_prompts):
+                ops.prompt_inject_fwd(x, deep_prompts[i - 1], N, L, self.row0, N_CTX, D)
+            h1 = self.H1
+            ops.layernorm_fwd(x, self.p(i, "ln_1.weight"), self.p(i, "ln_1.bias"), h1, self.mean1[i], self.rstd1[i])
+            ops.gemm_nt(h1, self.p(i, "attn.in_proj_weight"), self.QKV[i], bias=self.p(i, "attn.in_proj_bias"),
+                        epilogue=ops.EPI_BIAS)
+            ops.attention_fwd(self.QKV[i], N, L, H, self.causal, out=self.O[i], lse=self.LSE[i])
+            ops.gemm_nt(self.O[i], self.p(i, "attn.out_proj.weight"), self.X1[i], bias=self.p(i, "attn.out_proj.bias"),
+                        aux_in=x, epilogue=ops.EPI_BIAS_RESID)
+            h2 = self.H2
+            ops.layernorm_fwd(self.X1[i], self.p(i, "ln_2.weight"), self.p(i, "ln_2.bias"), h2, self.mean2[i],
+                              self.rstd2[i])
+            ops.gemm_nt(h2, self.p(i, "mlp.c_fc.weight"), self.G, bias=self.p(i, "mlp.c_fc.bias"), aux_out=self.Fp[i],
+                        epilogue=ops.EPI_BIAS_GELU)
+            ops.gemm_nt(self.G, self.p(i, "mlp.c_proj.weight"), self.X[i + 1], bias=self.p(i, "mlp.c_proj.bias"),
+                        aux_in=self.X1[i], epilogue=ops.EPI_BIAS_RESID)
+        # self.H1 / H2 / G now hold the last layer's (block 11) tensors, kept for its dW
+
+    def _dw(self, dY: torch.Tensor, Xin: torch.Tensor, dW: torch.Tensor, db: torch.Tensor):
+        """dW[out,in] = dY^T . Xin (fp16 out), db = colsum(dY)."""
+        R, Rp = self.R, self.Rp
+        o, k = dY.shape[1], Xin.shape[1]
+        ops.transpose(dY, self.tA[:o, :R])
+        ops.transpose(Xin, self.tB[:k, :R])
+        ops.gemm_nt(self.tA[:o], self.tB[:k], dW, epilogue=ops.EPI_NONE)
+        ops.colsum(dY, db, self.cs_ws)
+
+    def backward(self, n_prompted: int, prompt_grads: List[torch.Tensor]):
+        """self.dX holds d(loss)/d(X[layers]).  On return self.dX = d(loss)/d(X[0]) (the injected rows
+        of prompted layers reduced into prompt_grads[j] for the prompt injected before layer j+1)."""
+        N, L, D, H = self.N, self.L, self.D, self.H
+        dX = self.dX
+        last = self.layers - 1
+        for i in reversed(range(self.layers)):
+            trainable_w = i == last
+            # ---- MLP: X[i+1] = X1 + c_proj(gelu(c_fc(ln_2(X1))))
+            ops.gemm_nt(dX, self.wt(i, "mlp.c_proj.weight"), self.dF, aux_in=self.Fp[i], epilogue=ops.EPI_DGELU)
+            if trainable_w:
+                self._dw(dX, self.G, self.g(i, "mlp.c_proj.weight"), self.g(i, "mlp.c_proj.bias"))
+            ops.gemm_nt(self.dF, self.wt(i, "mlp.c_fc.weight"), self.dH, epilogue=ops.EPI_NONE)
+            if trainable_w:
+                self._dw(self.dF, self.H2, self.g(i, "mlp.c_fc.weight"), self.g(i, "mlp.c_fc.bias"))
+            ops.layernorm_bwd(self.dH, self.X1[i], self.p(i, "ln_2.weight"), self.mean2[i], self.rstd2[i], dX,
+                              self.g(i, "ln_2.weight"), self.g(i, "ln_2.bias"), self.ln_ws, dres=dX)
+            # ---- attention: X1 = X + out_proj(attn(ln_1(X)))
+            ops.gemm_nt(dX, self.wt(i, "attn.out_proj.weight"), self.dO, epilogue=ops.EPI_NONE)
+            if trainable_w:
+                self._dw(dX, self.O[i], self.g(i, "attn.out_proj.weight"), self.g(i, "attn.out_proj.bias"))
+            ops.attention_bwd(self.QKV[i], self.O[i], self.dO, self.LSE[i], N, L, H, self.causal, dqkv=self.dQKV,
+                              ws=self.attn_ws)
+            ops.gemm_nt(self.dQKV, self.wt(i, "attn.in_proj_weight"), self.dH, epilogue=ops.EPI_NONE)
+            if trainable_w:
+                self._dw(self.dQKV, self.H1, self.g(i, "attn.in_proj_weight"), self.g(i, "attn.in_proj_bias"))
+            ops.layernorm_bwd(self.dH, self.X[i], self.p(i, "ln_1.weight"), self.mean1[i], self.rstd1[i], dX,
+                              self.g(i, "ln_1.weight"), self.g(i, "ln_1.bias"), self.ln_ws, dres=dX)
+            if 1 <= i <= n_prompted:
+                ops.prompt_inject_bwd(dX, N, L, self.row0, N_CTX, D, prompt_grads[i - 1], accumulate=False,
+                                      zero_rows=True)
+
+
+class MapleEngine:
+    """One federated client on one GPU."""
+
+    def __init__(self, cfg: EngineConfig, device="cuda", state: Optional[Dict[str, np.ndarray]] = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        d = cfg.dims
+        self.B, self.K, self.J = cfg.batch, len(cfg.classnames), cfg.prompt_depth
+        assert 1 <= self.J <= 12, "PROMPT_DEPTH must be in [1, 12]"
+        self.specs = reference_param_specs(cfg)
+        vals = state if state is not None else synthetic_state(cfg)
+        self._build_params(vals)
+        self._build_text_constants()
+        G2 = d.grid * d.grid
+        self.Lv = G2 + 1 + cfg.n_ctx
+        self.G2 = G2
+        self.vis = _Tower(self, "image_encoder", self.B, self.Lv, d.vision_width, d.vision_heads, d.vision_layers,
+                          False, G2 + 1)
+        self.txt = _Tower(self, "text_encoder", self.K, d.context_length, d.text_width, d.text_heads, d.text_layers,
+                          True, 1)
+        self._build_io()
+        self.step_count = 0
+        self.hyper = torch.tensor([0.0, cfg.momentum, cfg.weight_decay, 1.0], device=self.device, dtype=F32)
+        self.momentum_initialised = False
+
+    # ------------------------------------------------------------------ parameters
+    def _build_params(self, vals: Dict[str, np.ndarray]):
+        dev = self.device
+        tr16 = [(n, s) for n, s, dt in self.specs if _is_trainable(n) and dt == F16 and "proj_vis_to_lang" not in n]
+        tr32 = [(n, s) for n, s, dt in self.specs if _is_trainable(n) and dt == F32]
+        n16 = sum(int(np.prod(s)) for _, s in tr16)
+        n32 = sum(int(np.prod(s)) for _, s in tr32)
+        self.n16, self.n32 = n16, n32
+        self.flat16 = torch.empty(n16, device=dev, dtype=F16)
+        self.flat32 = torch.empty(n32, device=dev, dtype=F32)
+        self.gflat16 = torch.zeros(n16, device=dev, dtype=F16)
+        self.gflat32 = torch.zeros(n32, device=dev, dtype=F32)
+        self.mom16 = torch.zeros(n16, device=dev, dtype=F16)
+        self.mom32 = torch.zeros(n32, device=dev, dtype=F32)
+        self.P: Dict[str, torch.Tensor] = {}
+        self.G: Dict[str, torch.Tensor] = {}
+        self.trainable_names: List[str] = []
+        segs = []  # (offset, numel, is16) per trainable tensor, in order
+        off = 0
+        for n, s in tr16:
+            k = int(np.prod(s))
+            self.P[n] = self.flat16[off:off + k].view(s)
+            self.G[n] = self.gflat16[off:off + k].view(s)
+            segs.append((off, k, 1))
+            self.trainable_names.append(n)
+            off += k
+        off = 0
+        for n, s in tr32:
+            k = int(np.prod(s))
+            self.P[n] = self.flat32[off:off + k].view(s)
+            self.G[n] = self.gflat32[off:off + k].view(s)
+            segs.append((off, k, 0))
+            self.trainable_names.append(n)
+            off += k
+        for n, s, dt in self.specs:
+            if n in self.P:
+                continue
+            self.P[n] = torch.empty(s, device=dev, dtype=dt)
+        for n, s, dt in self.specs:
+            v = vals[n]
+            assert tuple(v.shape) == tuple(s), (n, v.shape, s)
+            self.P[n].copy_(torch.from_numpy(np.ascontiguousarray(v).reshape(s)).to(dt))
+        # conv1 as a [768, 3*16*16] GEMM operand (im2col K order c, kh, kw)
+        cw = self.P["image_encoder.conv1.weight"]
+        self.conv_w = cw.view(cw.shape[0], -1)
+        # chunk table for clip_grad_norm (segments in trainable order; fp16 first then fp32)
+        ce = ops.optim_chunk_elems()
+        rows = []
+        for sid, (o, k, is16) in enumerate(segs):
+            for s0 in range(o, o + k, ce):
+                rows.append((sid, is16, s0, min(o + k, s0 + ce)))
+        arr = np.zeros(len(rows), dtype=np.dtype([("seg", np.int32), ("is16", np.int32), ("s", np.int64),
+                                                  ("e", np.int64)]))
+        for i, r in enumerate(rows):
+            arr[i] = r
+        self.chunks = torch.from_numpy(arr.view(np.uint8)).to(dev)
+        self.nchunks = len(rows)
+        self.norm_part = torch.empty(self.nchunks, device=dev, dtype=F32)
+        self.clip_out = torch.zeros(3, device=dev, dtype=F32)
+        # transposed weight copies for the dX products, and the transposed head projections
+        self.WT: Dict[str, torch.Tensor] = {}
+        for n, s, dt in self.specs:
+            if ".resblocks." in n and n.endswith(("in_proj_weight", "out_proj.weight", "c_fc.weight", "c_proj.weight")):
+                self.WT[n] = torch.empty(s[1], s[0], device=dev, dtype=F16)
+        self.refresh_transposes(all_layers=True)
+
+    def refresh_transposes(self, all_layers: bool = False):
+        """W^T copies feed the dX GEMMs; frozen blocks once, block 11 after every optimizer step."""
+        for n, t in self.WT.items():
+            if all_layers or ".resblocks.11." in n:
+                ops.transpose(self.P[n], t)
+        if all_layers:  # frozen head projections (x @ proj == NT GEMM with proj^T)
+            self.projT = self.P["image_encoder.proj"].t().contiguous()
+            self.text_projT = self.P["text_encoder.text_projection"].t().contiguous()
+
+    def _build_text_constants(self):
+        """token prefix / suffix buffers and the EOT gather index (trainers/maple.py:136-149)."""
+        cfg = self.cfg
+        texts = [f"{cfg.ctx_init} {c.replace('_', ' ')}." for c in cfg.classnames]
+        tok = syn.tokenize(texts)
+        self.tokenized = torch.from_numpy(tok)
+        emb = syn.token_embedding_rows(cfg.seed, tok.reshape(-1)).reshape(len(texts), 77, 512)
+        dev = self.device
+        self.token_prefix = torch.from_numpy(emb[:, :1]).to(dev, F16).contiguous()
+        self.token_suffix = torch.from_numpy(emb[:, 1 + cfg.n_ctx:]).to(dev, F16).contiguous()
+        eot = tok.argmax(axis=-1)
+        self.eot_rows = torch.from_numpy((np.arange(len(texts)) * 77 + eot).astype(np.int32)).to(dev)
+
+    def set_text_prompts(self, token_prefix: torch.Tensor, token_suffix: torch.Tensor, tokenized: torch.Tensor):
+        """Use real tokenizer output (prefix/suffix embeddings as the reference registers them)."""
+        self.token_prefix.copy_(token_prefix)
+        self.token_suffix.copy_(token_suffix)
+        eot = tokenized.argmax(dim=-1).cpu().numpy()
+        self.eot_rows.copy_(torch.from_numpy((np.arange(len(eot)) * 77 + eot).astype(np.int32)))
+
+    # ------------------------------------------------------------------ activations / io
+    def _build_io(self):
+        dev, B, K = self.device, self.B, self.K
+        d = self.cfg.dims
+        dv, dt, E = d.vision_width, d.text_width, d.embed_dim
+        J = self.J
+        e = lambda *s, dt_=F16: torch.empty(*s, device=dev, dtype=dt_)
+        self.img_in = e(B, 3, d.image_resolution, d.image_resolution, dt_=F32)
+        self.label_in = torch.zeros(B, device=dev, dtype=torch.int64)
+        self.im2col = e(B * self.G2, 3 * d.vision_patch ** 2)
+        self.patch = e(B * self.G2, dv)
+        self.Xpre = e(B * self.Lv, dv)
+        self.pre_mean, self.pre_rstd = e(B * self.Lv, dt_=F32), e(B * self.Lv, dt_=F32)
+        self.shared_ctx = e(N_CTX, dv)
+        self.vis_deep = [e(N_CTX, dv, dt_=F32) for _ in range(J - 1)]
+        self.txt_deep = [e(N_CTX, dt, dt_=F32) for _ in range(J - 1)]
+        self.g_vis_deep = [e(N_CTX, dv, dt_=F32) for _ in range(J - 1)]
+        self.g_txt_deep = [e(N_CTX, dt, dt_=F32) for _ in range(J - 1)]
+        self.g_shared_ctx = e(N_CTX, dv)
+        self.vis_post = e(B, dv)
+        self.post_mean, self.post_rstd = e(B, dt_=F32), e(B, dt_=F32)
+        self.cls_rows = torch.arange(0, B * self.Lv, self.Lv, dtype=torch.int32, device=dev)
+        self.img_feat = e(B, E)
+        self.txt_final = e(K, dt)
+        self.fin_mean, self.fin_rstd = e(K, dt_=F32), e(K, dt_=F32)
+        self.txt_feat = e(K, E)
+        self.img_n, self.txt_n = e(B, E), e(K, E)
+        self.norms = e(B + K, dt_=F32)
+        self.mm, self.logits, self.dmm = e(B, K), e(B, K), e(B, K)
+        self.cos_ws = e(2 * B, dt_=F32)
+        self.loss_out = torch.zeros(4, device=dev, dtype=F32)
+        self.dimg_n, self.dtxt_n = e(B, E), e(K, E)
+        self.dimg, self.dtxt = e(B, E), e(K, E)
+        self.d_vis_post, self.d_txt_final = e(B, dv), e(K, dt)
+        self.dXpre = e(B * self.Lv, dv)
+        self.ln_ws_small = e(max(ops.layernorm_ws_floats(max(B, K), dv), ops.layernorm_ws_floats(B * self.Lv, dv)),
+                             dt_=F32)
+
+    def load_batch(self, images: torch.Tensor, labels: Optional[torch.Tensor] = None):
+        """Copy a batch into the static input buffers (H2D when given host tensors)."""
+        self.img_in.copy_(images, non_blocking=True)
+        if labels is not None:
+            self.label_in.copy_(labels, non_blocking=True)
+
+    # ------------------------------------------------------------------ prompt learner
+    def _prompt_learner_fwd(self):
+        """MultiModalPromptLearner.forward (trainers/maple.py:177-218)."""
+        P = self.P
+        pl = "prompt_learner."
+        ops.small_linear_fwd(P[pl + "ctx"], P[pl + "proj_lang_to_vis.weight"], P[pl + "proj_lang_to_vis.bias"],
+                             self.shared_ctx)
+        for i in range(self.J - 1):
+            w = P[pl + f"compound_prompt_projections.{i}.weight"]
+            b = P[pl + f"compound_prompt_projections.{i}.bias"]
+            if i % 2 == 0:
+                t = P[pl + f"compound_prompts_text_parameters.{i // 2}"]
+                self.txt_deep[i].copy_(t)
+                ops.small_linear_fwd(t, w, b, self.vis_deep[i])
+            else:
+                v = P[pl + f"visual_deep_prompts_parameters.{(i - 1) // 2}"]
+                self.vis_deep[i].copy_(v)
+                ops.small_linear_fwd(v, w, b, self.txt_deep[i])
+
+    def _prompt_learner_bwd(self):
+        P, G = self.P, self.G
+        pl = "prompt_learner."
+        for i in range(self.J - 1):
+            w = P[pl + f"compound_prompt_projections.{i}.weight"]
+            dw = G[pl + f"compound_prompt_projections.{i}.weight"]
+            db = G[pl + f"compound_prompt_projections.{i}.bias"]
+            if i % 2 == 0:
+                name = pl + f"compound_prompts_text_parameters.{i // 2}"
+                G[name].copy_(self.g_txt_deep[i])          # direct use as the text prompt
+                ops.small_linear_bwd(self.g_vis_deep[i], P[name], w, G[name], dw, db, accumulate_dx=True)
+            else:
+                name = pl + f"visual_deep_prompts_parameters.{(i - 1) // 2}"
+                G[name].copy_(self.g_vis_deep[i])
+                ops.small_linear_bwd(self.g_txt_deep[i], P[name], w, G[name], dw, db, accumulate_dx=True)
+        # ctx: text-path grad (already in G[ctx]) + fp16(d shared_ctx . W)
+        ops.small_linear_bwd(self.g_shared_ctx, P[pl + "ctx"], P[pl + "proj_lang_to_vis.weight"], G[pl + "ctx"],
+                             G[pl + "proj_lang_to_vis.weight"], G[pl + "proj_lang_to_vis.bias"], accumulate_dx=True)
+
+    # ------------------------------------------------------------------ forward
+    def _text_forward(self):
+        P = self.P
+        t = self.txt
+        ops.text_assemble(self.token_prefix, P["prompt_learner.ctx"], self.token_suffix,
+                          P["text_encoder.positional_embedding"], t.X[0], self.K, t.L, N_CTX, t.D)
+        t.forward(self.txt_deep)
+        ops.layernorm_fwd(t.X[-1], P["text_encoder.ln_final.weight"], P["text_encoder.ln_final.bias"], self.txt_final,
+                          self.fin_mean, self.fin_rstd, row_index=self.eot_rows)
+        ops.gemm_nt(self.txt_final, self.text_projT, self.txt_feat, epilogue=ops.EPI_NONE)
+
+    def _vision_forward(self):
+        P = self.P
+        v = self.vis
+        ops.im2col_patch(self.img_in, self.im2col, self.cfg.dims.vision_patch)
+        ops.gemm_nt(self.im2col, self.conv_w, self.patch, epilogue=ops.EPI_NONE)
+        ops.vision_assemble(self.patch, P["image_encoder.class_embedding"], P["image_encoder.positional_embedding"],
+                            self.shared_ctx, self.Xpre, self.B, self.G2, N_CTX, v.D)
+        ops.layernorm_fwd(self.Xpre, P["image_encoder.ln_pre.weight"], P["image_encoder.ln_pre.bias"], v.X[0],
+                          self.pre_mean, self.pre_rstd)
+        v.forward(self.vis_deep)
+        ops.layernorm_fwd(v.X[-1], P["image_encoder.ln_post.weight"], P["image_encoder.ln_post.bias"], self.vis_post,
+                          self.post_mean, self.post_rstd, row_index=self.cls_rows)
+        ops.gemm_nt(self.vis_post, self.projT, self.img_feat, epilogue=ops.EPI_NONE)
+
+    def forward(self):
+        """CustomCLIP.forward up to the logits (eval path, trainers/maple.py:304-346)."""
+        self._prompt_learner_fwd()
+        self._text_forward()
+        self._vision_forward()
+        ops.clip_head_fwd(self.img_feat, self.txt_feat, self.P["logit_scale"], self.img_n, self.txt_n, self.norms,
+                          self.mm, self.logits)
+        return self.logits
+
+    # ------------------------------------------------------------------ backward
+    def _text_backward(self):
+        P, G = self.P, self.G
+        t = self.txt
+        ops.gemm_nt(self.dtxt, P["text_encoder.text_projection"], self.d_txt_final, epilogue=ops.EPI_NONE)
+        t.dX.zero_()
+        ops.layernorm_bwd(self.d_txt_final, t.X[-1], P["text_encoder.ln_final.weight"], self.fin_mean, self.fin_rstd,
+                          t.dX, G["text_encoder.ln_final.weight"], G["text_encoder.ln_final.bias"], self.ln_ws_small,
+                          row_index=self.eot_rows)
+        t.backward(self.J - 1, self.g_txt_deep)
+        # d ctx (text path): sum over classes of the rows 1..n_ctx of d prompts (fp16 result)
+        ops.prompt_inject_bwd(t.dX, self.K, t.L, 1, N_CTX, t.D, self.G["prompt_learner.ctx"], accumulate=False,
+                              zero_rows=False)
+
+    def _vision_backward(self):
+        P, G = self.P, self.G
+        v = self.vis
+        ops.gemm_nt(self.dimg, P["image_encoder.proj"], self.d_vis_post, epilogue=ops.EPI_NONE)
+        v.dX.zero_()
+        ops.layernorm_bwd(self.d_vis_post, v.X[-1], P["image_encoder.ln_post.weight"], self.post_mean,
+                          self.post_rstd, v.dX, G["image_encoder.ln_post.weight"], G["image_encoder.ln_post.bias"],
+                          self.ln_ws_small, row_index=self.cls_rows)
+        v.backward(self.J - 1, self.g_vis_deep)
+        ops.layernorm_bwd(v.dX, self.Xpre, P["image_encoder.ln_pre.weight"], self.pre_mean, self.pre_rstd, self.dXpre,
+                          G["image_encoder.ln_pre.weight"], G["image_encoder.ln_pre.bias"], self.ln_ws_small)
+        ops.prompt_inject_bwd(self.dXpre, self.B, self.Lv, self.G2 + 1, N_CTX, v.D, self.g_shared_ctx,
+                              accumulate=False, zero_rows=False)
+
+    def forward_backward(self):
+        """loss = CustomCLIP(image, label); loss.backward()  — grads land in gflat16/gflat32."""
+        self.forward()
+        ops.clip_loss_fwd_bwd(self.img_feat, self.txt_feat, self.img_n, self.txt_n, self.norms, self.logits,
+                              self.label_in, self.P["logit_scale"], self.dmm, self.cos_ws, self.loss_out,
+                              self.dimg_n, self.dtxt_n, self.dimg, self.dtxt)
+        self._text_backward()
+        self._vision_backward()
+        self._prompt_learner_bwd()
+
+    # ------------------------------------------------------------------ optimizer
+    def set_lr(self, lr: float):
+        self.hyper[0] = lr
+
+    def reset_momentum(self):
+        """broadcast_weights deletes the SGD state (trainers/maple_fed.py:331-335)."""
+        self.hyper[3] = 1.0
+
+    def optimizer_step(self):
+        """clip_grad_norm_(1.0) + SGD.step (trainers/maple.py:592-598), all on device."""
+        ops.clip_grad_norm(self.gflat16, self.gflat32, self.chunks, self.nchunks, self.cfg.max_grad_norm,
+                           self.norm_part, self.clip_out)
+        ops.sgd_step(self.flat16, self.gflat16, self.mom16, self.clip_out, self.hyper)
+        ops.sgd_step(self.flat32, self.gflat32, self.mom32, self.clip_out, self.hyper)
+        self.hyper[3] = 0.0
+        self.refresh_transposes(all_layers=False)
+
+    def train_step(self):
+        self.forward_backward()
+        self.optimizer_step()
+        self.step_count += 1
+
+    # ------------------------------------------------------------------ state
+    def loss(self) -> float:
+        v = self.loss_out.cpu()
+        if v[3].item() != 0.0:
+            raise RuntimeError("NaN/Inf in total loss")
+        return float(v[0])
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        return {n: t for n, t in self.P.items()}
+
+    def trainable_state(self) -> Dict[str, torch.Tensor]:
+        return {n: self.P[n] for n in self.trainable_names}
+
+    def grads(self) -> Dict[str, torch.Tensor]:
+        return {n: self.G[n] for n in self.trainable_names}

@@ -1,0 +1,194 @@
+"""Thin torch-tensor wrappers over the C ABI (include/mapfed.h).
+
+torch supplies device memory and the current HIP stream; every compute call goes through
+libmapfed.so.  Wrappers allocate outputs only when the caller passes none (the engine always
+passes preallocated buffers so a whole step can be captured in a hipGraph).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from ._lib import call
+
+EPI_NONE, EPI_BIAS, EPI_BIAS_RESID, EPI_BIAS_GELU, EPI_DGELU, EPI_F32, EPI_RESID = range(7)
+
+
+def _p(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _s():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ld(t: torch.Tensor) -> int:
+    assert t.dim() == 2 and t.stride(1) == 1, "row-major 2-D view required"
+    return t.stride(0)
+
+
+def gemm_nt(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NONE, tile=0):
+    """C[M,N] = epi(A[M,K] . B[N,K]^T)."""
+    M, K = A.shape
+    N, K2 = B.shape
+    assert K == K2, (A.shape, B.shape)
+    if C is None:
+        C = torch.empty(M, N, device=A.device, dtype=torch.float32 if epilogue == EPI_F32 else torch.float16)
+    aux = aux_in if aux_in is not None else aux_out
+    ld_aux = _ld(aux) if aux is not None else 0
+    call("mf_gemm_nt", _p(A), _ld(A), _p(B), _ld(B), _p(C), _ld(C), M, N, K, _p(bias), _p(aux_in), _p(aux_out),
+         ld_aux, epilogue, tile, _s())
+    return C
+
+
+def layernorm_fwd(x, gamma, beta, y=None, mean=None, rstd=None, row_index=None):
+    rows = row_index.numel() if row_index is not None else x.shape[0]
+    D = x.shape[1]
+    if y is None:
+        y = torch.empty(rows, D, device=x.device, dtype=torch.float16)
+    if mean is None:
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    if rstd is None:
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+    call("mf_layernorm_fwd", _p(x), _ld(x), _p(row_index), _p(gamma), _p(beta), _p(y), _ld(y), _p(mean), _p(rstd),
+         rows, D, _s())
+    return y, mean, rstd
+
+
+def layernorm_ws_floats(rows: int, D: int) -> int:
+    return 2 * call("mf_layernorm_bwd_blocks", rows) * D
+
+
+def layernorm_bwd(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, workspace=None, dres=None, row_index=None,
+                  accumulate=False):
+    rows, D = dy.shape
+    if workspace is None:
+        workspace = torch.empty(layernorm_ws_floats(rows, D), device=dy.device, dtype=torch.float32)
+    call("mf_layernorm_bwd", _p(dy), _ld(dy), _p(x), _ld(x), _p(row_index), _p(gamma), _p(mean), _p(rstd), _p(dres),
+         _ld(dres) if dres is not None else 0, _p(dx), _ld(dx), _p(dgamma), _p(dbeta), _p(workspace), rows, D,
+         int(accumulate), _s())
+    return dx
+
+
+def attention_fwd(qkv, N, L, H, causal, out=None, lse=None, ld_lse=None):
+    D = H * 64
+    if out is None:
+        out = torch.empty(N * L, D, device=qkv.device, dtype=torch.float16)
+    if ld_lse is None:
+        ld_lse = L
+    if lse is None:
+        lse = torch.empty(N * H * ld_lse, device=qkv.device, dtype=torch.float32)
+    call("mf_attention_fwd", _p(qkv), _ld(qkv), _p(out), _ld(out), _p(lse), ld_lse, N, L, H, int(causal), _s())
+    return out, lse
+
+
+def attention_bwd(qkv, out, dout, lse, N, L, H, causal, dqkv=None, ws=None, ld_lse=None):
+    if ld_lse is None:
+        ld_lse = L
+    if dqkv is None:
+        dqkv = torch.empty_like(qkv)
+    if ws is None:
+        ws = torch.empty(N * H * ld_lse, device=qkv.device, dtype=torch.float32)
+    call("mf_attention_bwd", _p(qkv), _ld(qkv), _p(out), _ld(out), _p(dout), _ld(dout), _p(lse), _p(ws), ld_lse,
+         _p(dqkv), _ld(dqkv), N, L, H, int(causal), _s())
+    return dqkv
+
+
+def im2col_patch(img, out, patch=16):
+    B, C, R, R2 = img.shape
+    assert C == 3 and R == R2 and img.is_contiguous()
+    call("mf_im2col_patch", _p(img), int(img.dtype == torch.float32), _p(out), B, R, patch, _s())
+    return out
+
+
+def vision_assemble(patch, cls, pos, shared_ctx, x, B, G2, n_ctx, D):
+    call("mf_vision_assemble", _p(patch), _p(cls), _p(pos), _p(shared_ctx), _p(x), B, G2, n_ctx, D, _s())
+    return x
+
+
+def text_assemble(prefix, ctx, suffix, pos, x, K, L, n_ctx, D):
+    call("mf_text_assemble", _p(prefix), _p(ctx), _p(suffix), _p(pos), _p(x), K, L, n_ctx, D, _s())
+    return x
+
+
+def prompt_inject_fwd(x, prompt, N, L, row0, nrows, D):
+    call("mf_prompt_inject_fwd", _p(x), _p(prompt), N, L, row0, nrows, D, _s())
+
+
+def prompt_inject_bwd(dx, N, L, row0, nrows, D, out, accumulate=False, zero_rows=True):
+    call("mf_prompt_inject_bwd", _p(dx), N, L, row0, nrows, D, _p(out), int(out.dtype == torch.float16),
+         int(accumulate), int(zero_rows), _s())
+
+
+def transpose(inp, out):
+    R, C = inp.shape
+    call("mf_transpose_f16", _p(inp), _ld(inp), _p(out), _ld(out), R, C, _s())
+    return out
+
+
+def colsum_ws_floats(R: int, C: int) -> int:
+    return call("mf_colsum_blocks", R) * C
+
+
+def colsum(inp, out, workspace=None):
+    R, C = inp.shape
+    if workspace is None:
+        workspace = torch.empty(colsum_ws_floats(R, C), device=inp.device, dtype=torch.float32)
+    call("mf_colsum_f16", _p(inp), _ld(inp), R, C, _p(out), int(out.dtype == torch.float16), _p(workspace), _s())
+    return out
+
+
+def small_linear_fwd(X, W, b, Y):
+    M, I = X.shape
+    O = W.shape[0]
+    call("mf_small_linear_fwd", _p(X), _p(W), _p(b), _p(Y), M, I, O, int(X.dtype == torch.float16), _s())
+    return Y
+
+
+def small_linear_bwd(dY, X, W, dX=None, dW=None, db=None, accumulate_dx=False):
+    M, I = X.shape
+    O = W.shape[0]
+    call("mf_small_linear_bwd", _p(dY), _p(X), _p(W), _p(dX), _p(dW), _p(db), M, I, O,
+         int(X.dtype == torch.float16), int(accumulate_dx), _s())
+
+
+def clip_head_fwd(img, txt, logit_scale, img_n, txt_n, norms, mm, logits):
+    B, D = img.shape
+    K = txt.shape[0]
+    call("mf_clip_head_fwd", _p(img), _p(txt), B, K, D, _p(logit_scale), _p(img_n), _p(txt_n), _p(norms), _p(mm),
+         _p(logits), _s())
+
+
+def clip_loss_fwd_bwd(img, txt, img_n, txt_n, norms, logits, label, logit_scale, dmm, cos_ws, loss_out, dimg_n,
+                      dtxt_n, dimg, dtxt):
+    B, D = img.shape
+    K = txt.shape[0]
+    call("mf_clip_loss_fwd_bwd", _p(img), _p(txt), _p(img_n), _p(txt_n), _p(norms), _p(logits), _p(label), B, K, D,
+         _p(logit_scale), _p(dmm), _p(cos_ws), _p(loss_out), _p(dimg_n), _p(dtxt_n), _p(dimg), _p(dtxt), _s())
+
+
+def optim_chunk_elems() -> int:
+    return call("mf_optim_chunk_elems")
+
+
+def clip_grad_norm(g16, g32, chunks, nchunks, max_norm, part, out):
+    call("mf_clip_grad_norm", _p(g16), _p(g32), _p(chunks), nchunks, float(max_norm), _p(part), _p(out), _s())
+
+
+def sgd_step(p, g, buf, coef, hyper):
+    """hyper: device fp32 tensor {lr, momentum, weight_decay, first_step}."""
+    call("mf_sgd_step", _p(p), _p(g), _p(buf), p.numel(), int(p.dtype == torch.float16), _p(coef), _p(hyper), _s())
+
+
+def fedavg_pack(p16, p32, bucket):
+    call("mf_fedavg_pack", _p(p16), p16.numel(), _p(p32), p32.numel(), _p(bucket), _s())
+
+
+def fedavg_unpack(bucket, n_valid, p16, p32):
+    call("mf_fedavg_unpack", _p(bucket), float(n_valid), _p(p16), p16.numel(), _p(p32), p32.numel(), _s())
+
+
+def nonfinite_flag(x, flag):
+    call("mf_nonfinite_flag", _p(x), x.numel(), int(x.dtype == torch.float16), _p(flag), _s())

@@ -1,0 +1,112 @@
+/*
+ * mapfed.h — C ABI of the MI355X-native federated MaPLe hot path (libmapfed.so, gfx950).
+ *
+ * The reference (tahaspc82442/federated_multi_modal) is pure Python on PyTorch: its "kernels" are
+ * implicit torch ops and it has no FFI below Python.  Each entry point
+ * below replaces the torch op(s) the reference calls at the cited file:line; INTEGRATION.md shows
+ * the ctypes binding and the Python module API (trainers/maple.py, trainers/maple_fed.py mirror)
+ * that sit on top.
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers owned by the caller (kernels never allocate or free).
+ *   - `stream` is a hipStream_t (void* so the header needs no HIP include); all work is enqueued
+ *     asynchronously on it; nothing synchronises the host.  Safe to capture in a hipGraph.
+ *   - fp16 tensors are IEEE binary16, row-major; `ld*` are leading dimensions in elements.
+ *   - Return value: 0 on success, non-zero on argument or launch error; the message is in
+ *     mf_last_error() (thread-local).
+ */
+#ifndef MAPFED_H_
+#define MAPFED_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* mf_last_error(void);
+int mf_abi_version(void);
+
+/* ---- dense projections (GEMM, MFMA) ------------------------------------------------------
+ * C[M,N] = epilogue(A[M,K] . B[N,K]^T), fp32 accumulate.  K % 64 == 0, N % 4 == 0.
+ * epilogue: 0 none | 1 +bias | 2 +bias then +aux_in residual | 3 +bias, aux_out = pre-activation,
+ *           C = QuickGELU | 4 C = QuickGELU'(fp16(acc), aux_in) | 5 fp32 store | 6 +aux_in residual
+ * tile: 0 auto, 1 128x128, 2 128x64, 3 64x64.
+ * Replaces: nn.Linear / addmm inside nn.MultiheadAttention in_proj + out_proj, mlp.c_fc, QuickGELU,
+ * mlp.c_proj and the residual adds (clip/model.py:274-280,303-305,350-351), the patch-embed conv as
+ * im2col GEMM (clip/model.py:514), the tower heads (clip/model.py:570, trainers/maple.py:76) and all
+ * of their autograd dX/dW products.                                                             */
+int mf_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
+               const void* bias, const void* aux_in, void* aux_out, int64_t ld_aux, int epilogue, int tile,
+               void* stream);
+
+/* ---- LayerNorm (fp16 io, fp32 math; clip/model.py:153-159) --------------------------------
+ * row_index (optional, int32): output row i normalises input row row_index[i]
+ * (ln_post on class tokens clip/model.py:567, ln_final + EOT gather trainers/maple.py:72-76).    */
+int mf_layernorm_fwd(const void* x, int64_t ldx, const int* row_index, const float* gamma, const float* beta,
+                     void* y, int64_t ldy, float* mean, float* rstd, int rows, int D, void* stream);
+/* dx = fp16(dres + fp16(LN'(dy)))  (dres optional; dx may alias dres); dgamma/dbeta written or
+ * accumulated (accumulate != 0).  workspace: 2 * mf_layernorm_bwd_blocks(rows) * D floats.        */
+int mf_layernorm_bwd_blocks(int rows);
+int mf_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const int* row_index,
+                     const float* gamma, const float* mean, const float* rstd, const void* dres, int64_t ldres,
+                     void* dx, int64_t lddx, float* dgamma, float* dbeta, float* workspace, int rows, int D,
+                     int accumulate, void* stream);
+
+/* ---- attention (head_dim 64, L <= 256; SDPA inside nn.MultiheadAttention, clip/model.py:303-305,
+ * causal mask clip/model.py:679-685) — qkv [N*L, 3*H*64], out [N*L, H*64], lse [N*H, ld_lse]       */
+int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* lse, int ld_lse, int N,
+                     int L, int H, int causal, void* stream);
+/* dqkv [N*L, 3*H*64]; dq_dot_ws: N*H*ld_lse floats of workspace                                   */
+int mf_attention_bwd(const void* qkv, int64_t ld_qkv, const void* out, int64_t ld_out, const void* dout,
+                     int64_t ld_dout, const float* lse, float* dq_dot_ws, int ld_lse, void* dqkv, int64_t ld_dqkv,
+                     int N, int L, int H, int causal, void* stream);
+
+/* ---- token assembly / prompt injection (clip/model.py:514-538,320-349; trainers/maple.py:54,152-166) */
+int mf_im2col_patch(const void* img, int img_is_f32, void* out, int B, int R, int P, void* stream);
+int mf_vision_assemble(const void* patch, const float* cls, const float* pos, const void* shared_ctx, void* x,
+                       int B, int G2, int n_ctx, int D, void* stream);
+int mf_text_assemble(const void* prefix, const void* ctx, const void* suffix, const float* pos, void* x, int K,
+                     int L, int n_ctx, int D, void* stream);
+int mf_prompt_inject_fwd(void* x, const float* prompt, int N, int L, int row0, int nrows, int D, void* stream);
+/* out[r,:] (=|+=) sum_n dx[n*L+row0+r,:] (fp32 accumulate, fp16 or fp32 out); zero_rows clears them  */
+int mf_prompt_inject_bwd(void* dx, int N, int L, int row0, int nrows, int D, void* out, int out_f16, int accumulate,
+                         int zero_rows, void* stream);
+
+/* ---- helpers for the backward products ------------------------------------------------------ */
+int mf_transpose_f16(const void* in, int64_t ld_in, void* out, int64_t ld_out, int R, int C, void* stream);
+int mf_colsum_blocks(int R);
+/* out[c] = sum_r in[r,c]; workspace: mf_colsum_blocks(R) * C floats                               */
+int mf_colsum_f16(const void* in, int64_t ld, int R, int C, void* out, int out_f16, float* workspace, void* stream);
+int mf_cast_f16_f32(const void* in, float* out, int64_t n, void* stream);
+
+/* ---- prompt-learner linears, M <= 16 rows (trainers/maple.py:111-131,194-215) --------------- */
+int mf_small_linear_fwd(const void* X, const void* W, const void* b, void* Y, int M, int I, int O, int is_f16,
+                        void* stream);
+int mf_small_linear_bwd(const void* dY, const void* X, const void* W, void* dX, void* dW, void* db, int M, int I,
+                        int O, int is_f16, int accumulate_dx, void* stream);
+
+/* ---- cosine-logit head + loss (trainers/maple.py:325,340-378) -------------------------------- */
+int mf_clip_head_fwd(const void* img, const void* txt, int B, int K, int D, const float* logit_scale, void* img_n,
+                     void* txt_n, float* norms, void* mm, void* logits, void* stream);
+int mf_clip_loss_fwd_bwd(const void* img, const void* txt, const void* img_n, const void* txt_n, const float* norms,
+                         const void* logits, const int64_t* label, int B, int K, int D, const float* logit_scale,
+                         void* dmm, float* cos_ws, float* loss_out, void* dimg_n, void* dtxt_n, void* dimg,
+                         void* dtxt, void* stream);
+
+/* ---- optimizer / federated averaging (trainers/maple.py:592-598; trainers/maple_fed.py:309-325) */
+int mf_optim_chunk_bytes(void);
+int mf_optim_chunk_elems(void);
+int mf_clip_grad_norm(const void* g16, const float* g32, const void* chunks, int nchunks, float max_norm,
+                      float* part, float* out, void* stream);
+/* coef: the clip output (coef at [1]); hyper (device): {lr, momentum, weight_decay, first_step}   */
+int mf_sgd_step(void* p, void* g, void* buf, int64_t n, int is16, const float* coef, const float* hyper,
+                void* stream);
+int mf_fedavg_pack(const void* p16, int64_t n16, const float* p32, int64_t n32, float* bucket, void* stream);
+int mf_fedavg_unpack(const float* bucket, float n_valid, void* p16, int64_t n16, float* p32, int64_t n32,
+                     void* stream);
+int mf_nonfinite_flag(const void* x, int64_t n, int is16, int* flag, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAPFED_H_ */

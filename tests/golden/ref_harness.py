@@ -1,0 +1,191 @@
+"""Import the reference's own MaPLe code (read-only, /root/reference) for golden fixtures.
+
+Runs ONLY in the build container (the reference never travels to the GPU box).
+How:
+  * clip/model.py is loaded by file path (its package __init__ needs torchvision);
+  * trainers/maple.py and trainers/maple_fed.py are loaded after stub modules for the
+    absent third-party pieces: Dassl (registry/TrainerX/optim/utils), the `clip`
+    package (tokenize -> the build's synthetic tokenizer) and SimpleTokenizer (the
+    BPE vocab file is absent).
+Nothing from the reference is copied; this module only wires imports.
+"""
+from __future__ import annotations
+
+import importlib.util
+import sys
+import types
+from pathlib import Path
+
+import numpy as np
+import torch
+
+REF = Path("/root/reference")
+REPO = Path(__file__).resolve().parents[2]
+if str(REPO) not in sys.path:
+    sys.path.insert(0, str(REPO))
+
+from federated_multi_modal_amd import synthetic as syn  # noqa: E402
+
+
+def _load(name: str, path: Path):
+    spec = importlib.util.spec_from_file_location(name, str(path))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+_CACHE = {}
+
+
+def load_reference():
+    if "maple" in _CACHE:
+        return _CACHE["model"], _CACHE["maple"], _CACHE["maple_fed"]
+    if not REF.exists():
+        raise RuntimeError("/root/reference is not present (golden generation runs in the build container only)")
+
+    # ---- Dassl stubs (un-vendored third party) ----
+    dassl = types.ModuleType("dassl")
+    engine = types.ModuleType("dassl.engine")
+
+    class _Registry:
+        def register(self):
+            return lambda cls: cls
+
+    class TrainerX:  # minimal base; the harness never calls TrainerX.__init__
+        def __init__(self, *a, **k):
+            pass
+
+    engine.TRAINER_REGISTRY = _Registry()
+    engine.TrainerX = TrainerX
+    metrics = types.ModuleType("dassl.metrics")
+    metrics.compute_accuracy = lambda *a, **k: None
+    utils = types.ModuleType("dassl.utils")
+    utils.load_pretrained_weights = lambda *a, **k: None
+    utils.load_checkpoint = lambda *a, **k: None
+    utils.mkdir_if_missing = lambda *a, **k: None
+    utils.save_checkpoint = lambda *a, **k: None
+    optim = types.ModuleType("dassl.optim")
+    optim.build_optimizer = lambda *a, **k: None
+    optim.build_lr_scheduler = lambda *a, **k: None
+    data = types.ModuleType("dassl.data")
+    data.DataManager = object
+    datasets = types.ModuleType("dassl.data.datasets")
+    datasets.Datum = object
+    dm = types.ModuleType("dassl.data.data_manager")
+    dm.build_transform = lambda *a, **k: None
+    dm.build_data_loader = lambda *a, **k: None
+    for m, n in [(dassl, "dassl"), (engine, "dassl.engine"), (metrics, "dassl.metrics"), (utils, "dassl.utils"),
+                 (optim, "dassl.optim"), (data, "dassl.data"), (datasets, "dassl.data.datasets"),
+                 (dm, "dassl.data.data_manager")]:
+        sys.modules[n] = m
+    dassl.engine, dassl.metrics, dassl.utils, dassl.optim, dassl.data = engine, metrics, utils, optim, data
+    data.datasets = datasets
+
+    # ---- clip package stub: reference model.py + synthetic tokenizer ----
+    model = _load("ref_clip_model", REF / "clip" / "model.py")
+    clip_pkg = types.ModuleType("clip")
+    clip_pkg.__path__ = []
+    clip_mod = types.ModuleType("clip.clip")
+    clip_mod.tokenize = lambda texts, context_length=77, truncate=False: torch.from_numpy(
+        syn.tokenize(texts, context_length))
+    clip_mod.build_model = model.build_model
+    clip_mod._MODELS = {}
+    st = types.ModuleType("clip.simple_tokenizer")
+
+    class SimpleTokenizer:
+        def encode(self, text):
+            return syn.encode(text)
+
+    st.SimpleTokenizer = SimpleTokenizer
+    clip_pkg.clip = clip_mod
+    clip_pkg.model = model
+    clip_pkg.simple_tokenizer = st
+    sys.modules["clip"] = clip_pkg
+    sys.modules["clip.clip"] = clip_mod
+    sys.modules["clip.model"] = model
+    sys.modules["clip.simple_tokenizer"] = st
+
+    # tqdm / PIL used by maple_fed at import time
+    for opt in ("tqdm", "PIL"):
+        try:
+            __import__(opt)
+        except Exception:  # pragma: no cover
+            stub = types.ModuleType(opt)
+            if opt == "tqdm":
+                stub.trange = range
+            else:
+                stub.Image = None
+            sys.modules[opt] = stub
+
+    maple = _load("ref_trainers_maple", REF / "trainers" / "maple.py")
+    trainers_pkg = types.ModuleType("trainers")
+    trainers_pkg.__path__ = []
+    trainers_pkg.maple = maple
+    sys.modules["trainers"] = trainers_pkg
+    sys.modules["trainers.maple"] = maple
+    cdm = types.ModuleType("trainers.client_datamanager")
+    cdm.ClientDataManager = object
+    sys.modules["trainers.client_datamanager"] = cdm
+    # maple_fed does `from .client_datamanager import ...`: give it a package context
+    spec = importlib.util.spec_from_file_location("trainers.maple_fed", str(REF / "trainers" / "maple_fed.py"))
+    maple_fed = importlib.util.module_from_spec(spec)
+    maple_fed.__package__ = "trainers"
+    sys.modules["trainers.maple_fed"] = maple_fed
+    spec.loader.exec_module(maple_fed)
+
+    _CACHE.update(model=model, maple=maple, maple_fed=maple_fed)
+    return model, maple, maple_fed
+
+
+class _NS:
+    def __init__(self, **kw):
+        for k, v in kw.items():
+            setattr(self, k, _NS(**v) if isinstance(v, dict) else v)
+
+
+def make_cfg(prompt_depth: int, n_ctx: int = 2, ctx_init: str = "a photo of a"):
+    return _NS(TRAINER={"MAPLE": {"N_CTX": n_ctx, "CTX_INIT": ctx_init, "PREC": "fp16",
+                                  "PROMPT_DEPTH": prompt_depth}},
+               INPUT={"SIZE": (224, 224)})
+
+
+def build_reference_model(seed: int, prompt_depth: int, classnames, vision_layers: int = 12,
+                          text_layers: int = 12):
+    """CustomCLIP exactly as MaPLe.build_model builds it (trainers/maple.py:421-479), with
+    synthetic weights in place of the downloaded checkpoint."""
+    model_mod, maple, _ = load_reference()
+    dims = syn.ClipDims()
+    sd = syn.clip_state_dict(seed, dims, full_token_table=True, vision_layers=vision_layers,
+                             text_layers=text_layers)
+    design = {"trainer": "MaPLe", "vision_depth": 0, "language_depth": 0, "vision_ctx": 0,
+              "language_ctx": 0, "maple_length": 2}
+    clip_model = model_mod.CLIP(dims.embed_dim, dims.image_resolution, vision_layers, dims.vision_width,
+                                dims.vision_patch, dims.context_length, dims.vocab_size, dims.text_width,
+                                dims.text_heads, text_layers, design)
+    model_mod.convert_weights(clip_model)
+    tsd = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd.items()}
+    clip_model.load_state_dict(tsd, strict=True)  # load_state_dict keeps each param's dtype
+    clip_model.eval()
+    cfg = make_cfg(prompt_depth)
+    torch.manual_seed(seed)
+    model = maple.CustomCLIP(cfg, list(classnames), clip_model)
+    pl = syn.prompt_learner_params(seed, prompt_depth)
+    with torch.no_grad():
+        for k, v in pl.items():
+            p = dict(model.prompt_learner.named_parameters())[k]
+            p.copy_(torch.from_numpy(v).to(p.dtype))
+    # freeze policy, restated from trainers/maple.py:447-479
+    for p in model.parameters():
+        p.requires_grad_(False)
+    for _, mod in model.named_modules():
+        if isinstance(mod, (torch.nn.LayerNorm, torch.nn.BatchNorm1d, torch.nn.BatchNorm2d)):
+            for p in mod.parameters():
+                p.requires_grad_(True)
+    for n, p in model.named_parameters():
+        if "prompt_learner" in n:
+            p.requires_grad_(True)
+    for n, p in model.named_parameters():
+        if "visual.transformer.resblocks.11" in n or "transformer.resblocks.11" in n:
+            p.requires_grad_(True)
+    return model

@@ -1,0 +1,327 @@
+"""Per-kernel numerics of libmapfed.so on the MI355X, each against a plain PyTorch fp32 (or fp64)
+reference of the same op.  Tolerances are written per test; fp16 outputs are compared in units of
+the fp16 ulp of the reference value."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from federated_multi_modal_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def ulp16(x: torch.Tensor) -> torch.Tensor:
+    a = x.abs().float().clamp_min(2.0 ** -14)
+    return torch.exp2(torch.floor(torch.log2(a)) - 10)
+
+
+def assert_ulps(out, ref, max_ulp=1.0, frac=1e-2, what="", floor=2e-5):
+    """|out - ref| <= max_ulp fp16 ulps of the reference value, with an absolute floor of
+    floor*max|ref| for values near zero (where fp32 accumulation order, not the fp16 rounding,
+    sets the error); at most `frac` of elements off by more than half an ulp."""
+    unit = torch.maximum(ulp16(ref), torch.tensor(floor * ref.abs().max().item(), device=ref.device))
+    d = (out.float() - ref.float()).abs() / unit
+    worst = d.max().item()
+    bad = (d > 0.51).float().mean().item()
+    assert worst <= max_ulp + 1e-6, f"{what}: worst {worst:.2f} ulp"
+    assert bad <= frac, f"{what}: {bad:.4f} of elements beyond half an ulp"
+
+
+@pytest.mark.parametrize("M,N,K,tile", [(796, 2304, 768, 0), (6368, 768, 3072, 0), (770, 512, 2048, 1),
+                                        (130, 44, 64, 3), (257, 1536, 512, 2), (6368, 3072, 768, 0)])
+def test_gemm_bias(dev, M, N, K, tile):
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).half().to(dev)
+    B = (torch.randn(N, K, generator=g) * K ** -0.5).half().to(dev)
+    b = (torch.randn(N, generator=g) * 0.1).half().to(dev)
+    C = ops.gemm_nt(A, B, bias=b, epilogue=ops.EPI_BIAS, tile=tile)
+    ref = (A.double() @ B.double().t() + b.double())
+    assert_ulps(C, ref, 1.0, 2e-2, "gemm+bias")
+    # no-bias and fp32 epilogues
+    C0 = ops.gemm_nt(A, B, epilogue=ops.EPI_NONE, tile=tile)
+    assert_ulps(C0, A.double() @ B.double().t(), 1.0, 2e-2, "gemm")
+    C32 = ops.gemm_nt(A, B, epilogue=ops.EPI_F32, tile=tile)
+    torch.testing.assert_close(C32.double(), A.double() @ B.double().t(), rtol=1e-5, atol=1e-4)
+
+
+def _gelu16(f):
+    t1 = (f.float() * 1.702).half()
+    t2 = torch.sigmoid(t1.float()).half()
+    return (f.float() * t2.float()).half()
+
+
+def test_gemm_epilogues(dev):
+    torch.manual_seed(0)
+    M, N, K = 600, 1024, 256
+    A = torch.randn(M, K).half().to(dev)
+    B = (torch.randn(N, K) * K ** -0.5).half().to(dev)
+    b = (torch.randn(N) * 0.1).half().to(dev)
+    R = torch.randn(M, N).half().to(dev)
+    acc = A.double() @ B.double().t()
+    y16 = (acc + b.double()).half()
+    # residual
+    C = ops.gemm_nt(A, B, bias=b, aux_in=R, epilogue=ops.EPI_BIAS_RESID)
+    ref = (R.float() + y16.float()).half()
+    assert (C.float() - ref.float()).abs().max().item() <= 2 * ulp16(ref).max().item()
+    assert (C != ref).float().mean().item() < 2e-2
+    # residual in place (C aliases R)
+    R2 = R.clone()
+    ops.gemm_nt(A, B, C=R2, bias=b, aux_in=R2, epilogue=ops.EPI_BIAS_RESID)
+    assert torch.equal(R2, C)
+    # gelu: stores pre-activation and QuickGELU with the reference's roundings
+    Fpre = torch.empty(M, N, dtype=torch.float16, device=dev)
+    G = ops.gemm_nt(A, B, bias=b, aux_out=Fpre, epilogue=ops.EPI_BIAS_GELU)
+    assert (Fpre != y16).float().mean().item() < 2e-2
+    assert (G != _gelu16(Fpre)).float().mean().item() < 1e-3
+    # dgelu: the reference's autograd of QuickGELU on CPU torch (sigmoid_backward for Half runs in
+    # fp16 op by op there), restated with explicit ops on the kernel's own fp16 GEMM output
+    dG = ops.gemm_nt(A, B, aux_in=Fpre, epilogue=ops.EPI_DGELU)
+    dg = ops.gemm_nt(A, B, epilogue=ops.EPI_NONE).float()
+    h = lambda t: t.half().float()
+    ff = Fpre.float()
+    t2 = h(torch.sigmoid(h(ff * 1.702)))
+    dt1 = h(h(h(dg * ff) * h(1 - t2)) * t2)
+    man = (h(dg * t2) + h(dt1 * 1.702)).half()
+    assert (dG != man).float().mean().item() < 1e-3
+    # and within 2 ulp of GPU torch's own fp16 autograd (which computes sigmoid_backward in fp32)
+    f = Fpre.clone().requires_grad_(True)
+    (f * torch.sigmoid(1.702 * f)).backward(dg.half())
+    assert_ulps(dG, f.grad.double(), 2.0, 0.5, "dgelu vs torch-gpu autograd", floor=1e-3)
+
+
+@pytest.mark.parametrize("D,rows", [(768, 6368), (512, 770), (768, 5)])
+def test_layernorm(dev, D, rows):
+    torch.manual_seed(D + rows)
+    x = (torch.randn(rows, D) * 2 + 0.5).half().to(dev)
+    g = (1 + 0.1 * torch.randn(D)).to(dev)
+    b = (0.1 * torch.randn(D)).to(dev)
+    y, mean, rstd = ops.layernorm_fwd(x, g, b)
+    ref = F.layer_norm(x.double(), (D,), g.double(), b.double(), 1e-5)
+    assert_ulps(y, ref, 1.0, 1e-2, "ln fwd")
+    # backward vs autograd fp64, with residual accumulation
+    dy = torch.randn(rows, D).half().to(dev)
+    dres = torch.randn(rows, D).half().to(dev)
+    xx = x.double().requires_grad_(True)
+    gg = g.double().requires_grad_(True)
+    bb = b.double().requires_grad_(True)
+    F.layer_norm(xx, (D,), gg, bb, 1e-5).backward(dy.double())
+    dx = torch.empty_like(x)
+    dg = torch.empty(D, device=dev)
+    db = torch.empty(D, device=dev)
+    ops.layernorm_bwd(dy, x, g, mean, rstd, dx, dg, db, dres=dres)
+    refdx = (dres.double() + xx.grad.half().double())
+    assert (dx.float() - refdx.float()).abs().max().item() <= 2 * ulp16(refdx).max().item()
+    torch.testing.assert_close(dg.double(), gg.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db.double(), bb.grad, rtol=1e-4, atol=1e-3)
+
+
+def test_layernorm_row_index(dev):
+    torch.manual_seed(1)
+    D, R = 768, 4 * 199
+    x = torch.randn(R, D).half().to(dev)
+    idx = torch.arange(0, R, 199, dtype=torch.int32, device=dev)
+    g = torch.ones(D, device=dev)
+    b = torch.zeros(D, device=dev)
+    y, mean, rstd = ops.layernorm_fwd(x, g, b, row_index=idx)
+    ref = F.layer_norm(x[idx.long()].double(), (D,), g.double(), b.double(), 1e-5)
+    assert_ulps(y, ref, 1.0, 1e-2, "ln gather")
+    dy = torch.randn(4, D).half().to(dev)
+    dx = torch.zeros_like(x)
+    dg = torch.empty(D, device=dev)
+    db = torch.empty(D, device=dev)
+    ops.layernorm_bwd(dy, x, g, mean, rstd, dx, dg, db, row_index=idx)
+    mask = torch.ones(R, dtype=torch.bool, device=dev)
+    mask[idx.long()] = False
+    assert dx[mask].abs().max().item() == 0
+
+
+def _attn_ref(q, k, v, causal):
+    """fp64 restatement of the kernel's numerics: P = exp(s - max) rounded to fp16, sum unrounded."""
+    s = (q.double() @ k.double().transpose(-1, -2)) * 0.125
+    if causal:
+        L = s.shape[-1]
+        s = s + torch.full((L, L), float("-inf"), device=s.device, dtype=s.dtype).triu(1)
+    m = s.max(-1, keepdim=True).values
+    e = torch.exp(s - m)
+    return (e.half().double() @ v.double()) / e.sum(-1, keepdim=True)
+
+
+@pytest.mark.parametrize("N,L,H,causal", [(4, 199, 12, False), (10, 77, 8, True), (3, 50, 2, False),
+                                          (2, 256, 4, True)])
+def test_attention_fwd_bwd(dev, N, L, H, causal):
+    torch.manual_seed(L)
+    D = H * 64
+    qkv = torch.randn(N * L, 3 * D).half().to(dev)
+    out, lse = ops.attention_fwd(qkv, N, L, H, causal)
+    q, k, v = qkv.view(N, L, 3, H, 64).permute(2, 0, 3, 1, 4).unbind(0)  # [N,H,L,64]
+    ref = _attn_ref(q, k, v, causal).permute(0, 2, 1, 3).reshape(N * L, D)
+    assert_ulps(out, ref, 4.0, 2e-2, "attn fwd")
+    # torch SDPA (the reference's op) within 1e-3 absolute
+    mask = None
+    if causal:
+        mask = torch.full((L, L), float("-inf"), device=dev).triu(1).half()
+    sd = F.scaled_dot_product_attention(q, k, v, attn_mask=mask).permute(0, 2, 1, 3).reshape(N * L, D)
+    assert (out.float() - sd.float()).abs().max().item() < 2e-3
+    # backward vs autograd fp32
+    dout = torch.randn(N * L, D).half().to(dev)
+    dqkv = ops.attention_bwd(qkv, out, dout, lse, N, L, H, causal)
+    qq, kk, vv = [t.float().detach().requires_grad_(True) for t in (q, k, v)]
+    m32 = mask.float() if mask is not None else None
+    o32 = F.scaled_dot_product_attention(qq, kk, vv, attn_mask=m32)
+    o32.backward(dout.float().view(N, L, H, 64).permute(0, 2, 1, 3))
+    gref = torch.stack([qq.grad, kk.grad, vv.grad], 0).permute(1, 3, 0, 2, 4).reshape(N * L, 3 * D)
+    err = (dqkv.float() - gref).abs()
+    scale = gref.abs().max().item()
+    assert err.max().item() < 1e-2 * scale + 2e-3, (err.max().item(), scale)
+    rel = err.norm().item() / gref.norm().item()
+    assert rel < 5e-3, rel
+
+
+def test_assemble_inject_transpose_colsum(dev):
+    torch.manual_seed(3)
+    B, G2, D, n_ctx = 3, 196, 768, 2
+    patch = torch.randn(B * G2, D).half().to(dev)
+    cls = torch.randn(D).to(dev)
+    pos = torch.randn(G2 + 1, D).to(dev)
+    sc = torch.randn(n_ctx, D).half().to(dev)
+    L = G2 + 1 + n_ctx
+    x = torch.empty(B * L, D, dtype=torch.float16, device=dev)
+    ops.vision_assemble(patch, cls, pos, sc, x, B, G2, n_ctx, D)
+    ref = torch.cat([cls.half().expand(B, 1, D) + torch.zeros(B, 1, D, dtype=torch.float16, device=dev),
+                     patch.view(B, G2, D)], 1) + pos.half()
+    ref = torch.cat([ref, sc.expand(B, -1, -1)], 1).reshape(B * L, D)
+    assert torch.equal(x, ref)
+    # inject + its backward
+    pr = torch.randn(n_ctx, D).to(dev)
+    ops.prompt_inject_fwd(x, pr, B, L, L - n_ctx, n_ctx, D)
+    assert torch.equal(x.view(B, L, D)[:, L - n_ctx:], pr.half().expand(B, -1, -1))
+    dx = torch.randn(B * L, D).half().to(dev)
+    d0 = dx.view(B, L, D)[:, L - n_ctx:].float().sum(0)
+    out = torch.empty(n_ctx, D, device=dev)
+    ops.prompt_inject_bwd(dx, B, L, L - n_ctx, n_ctx, D, out)
+    torch.testing.assert_close(out, d0, rtol=1e-6, atol=1e-6)
+    assert dx.view(B, L, D)[:, L - n_ctx:].abs().max().item() == 0
+    # text assemble
+    K, Lt, Dt = 5, 77, 512
+    prefix = torch.randn(K, 1, Dt).half().to(dev)
+    ctx = torch.randn(n_ctx, Dt).half().to(dev)
+    suffix = torch.randn(K, Lt - 1 - n_ctx, Dt).half().to(dev)
+    post = torch.randn(Lt, Dt).to(dev)
+    xt = torch.empty(K * Lt, Dt, dtype=torch.float16, device=dev)
+    ops.text_assemble(prefix, ctx, suffix, post, xt, K, Lt, n_ctx, Dt)
+    reft = (torch.cat([prefix, ctx.expand(K, -1, -1), suffix], 1) + post.half()).reshape(K * Lt, Dt)
+    assert torch.equal(xt, reft)
+    # transpose / colsum
+    a = torch.randn(300, 200).half().to(dev)
+    t = torch.zeros(200, 320, dtype=torch.float16, device=dev)
+    ops.transpose(a, t[:, :300])
+    assert torch.equal(t[:, :300], a.t()) and t[:, 300:].abs().max().item() == 0
+    cs = torch.empty(200, dtype=torch.float16, device=dev)
+    ops.colsum(a, cs)
+    assert (cs.float() - a.float().sum(0).half().float()).abs().max().item() <= ulp16(cs).max().item()
+
+
+def test_small_linear(dev):
+    torch.manual_seed(4)
+    for dt in (torch.float32, torch.float16):
+        X = torch.randn(2, 512, dtype=dt, device=dev)
+        W = (torch.randn(768, 512) * 0.05).to(dt).to(dev)
+        b = torch.randn(768, dtype=dt, device=dev)
+        Y = torch.empty(2, 768, dtype=dt, device=dev)
+        ops.small_linear_fwd(X, W, b, Y)
+        ref = F.linear(X.double(), W.double(), b.double())
+        tol = 1e-5 if dt == torch.float32 else 2e-3
+        torch.testing.assert_close(Y.double(), ref, rtol=tol, atol=tol)
+        dY = torch.randn(2, 768, dtype=dt, device=dev)
+        dX = torch.empty_like(X)
+        dW = torch.empty_like(W)
+        db = torch.empty_like(b)
+        ops.small_linear_bwd(dY, X, W, dX, dW, db)
+        torch.testing.assert_close(dX.double(), dY.double() @ W.double(), rtol=tol * 5, atol=tol * 5)
+        torch.testing.assert_close(dW.double(), dY.double().t() @ X.double(), rtol=tol * 5, atol=tol * 5)
+        torch.testing.assert_close(db.double(), dY.double().sum(0), rtol=tol * 5, atol=tol * 5)
+
+
+def test_clip_head_loss(dev):
+    torch.manual_seed(5)
+    B, K, D = 8, 38, 512
+    img = torch.randn(B, D).half().to(dev)
+    txt = torch.randn(K, D).half().to(dev)
+    label = torch.randint(0, K, (B,)).to(dev)
+    ls = torch.tensor([math.log(1 / 0.07)], device=dev)
+    img_n = torch.empty_like(img)
+    txt_n = torch.empty_like(txt)
+    norms = torch.empty(B + K, device=dev)
+    mm = torch.empty(B, K, dtype=torch.float16, device=dev)
+    logits = torch.empty_like(mm)
+    ops.clip_head_fwd(img, txt, ls, img_n, txt_n, norms, mm, logits)
+    # reference ops on the GPU in fp16 (trainers/maple.py:325,340-346)
+    i_ = img.clone().requires_grad_(True)
+    t_ = txt.clone().requires_grad_(True)
+    inr = F.normalize(i_, dim=-1, eps=1e-8)
+    tnr = F.normalize(t_, dim=-1, eps=1e-8)
+    ref_logits = ls.exp().clamp(max=100) * (inr @ tnr.t())
+    assert (logits.float() - ref_logits.float()).abs().max().item() <= 2e-2 * 1.0 + 1e-3
+    dmm = torch.empty_like(mm)
+    cos_ws = torch.empty(2 * B, device=dev)
+    loss = torch.empty(4, device=dev)
+    dimg_n, dtxt_n = torch.empty_like(img), torch.empty_like(txt)
+    dimg, dtxt = torch.empty_like(img), torch.empty_like(txt)
+    ops.clip_loss_fwd_bwd(img, txt, img_n, txt_n, norms, logits, label, ls, dmm, cos_ws, loss, dimg_n, dtxt_n,
+                          dimg, dtxt)
+    # fp32 reference of the loss and its gradient
+    i32 = img.float().requires_grad_(True)
+    t32 = txt.float().requires_grad_(True)
+    a = F.normalize(i32, dim=-1, eps=1e-8)
+    t = F.normalize(t32, dim=-1, eps=1e-8)
+    lg = ls.exp().clamp(max=100) * (a @ t.t())
+    tot = F.cross_entropy(lg, label) + 0.5 * (1 - F.cosine_similarity(a, t[label]).mean())
+    tot.backward()
+    assert abs(loss[0].item() - tot.item()) < 5e-3
+    torch.testing.assert_close(dimg.float(), i32.grad, rtol=2e-2, atol=2e-4)
+    torch.testing.assert_close(dtxt.float(), t32.grad, rtol=2e-2, atol=2e-4)
+
+
+def test_sgd_and_clip(dev):
+    torch.manual_seed(6)
+    n16, n32 = 10000, 5000
+    p16 = torch.randn(n16).half().to(dev)
+    p32 = torch.randn(n32).to(dev)
+    g16 = (torch.randn(n16) * 0.05).half().to(dev)
+    g32 = (torch.randn(n32) * 0.05).to(dev)
+    # reference: torch clip_grad_norm_ + SGD on copies
+    rp16 = p16.clone().requires_grad_(True)
+    rp32 = p32.clone().requires_grad_(True)
+    rp16.grad = g16.clone()
+    rp32.grad = g32.clone()
+    torch.nn.utils.clip_grad_norm_([rp16, rp32], 1.0)
+    opt = torch.optim.SGD([rp16, rp32], lr=0.01, momentum=0.9, weight_decay=5e-4, foreach=False)
+    opt.step()
+    # ours: segments = two tensors of each flat buffer
+    import ctypes
+    import numpy as np
+    ce = ops.optim_chunk_elems()
+    chunks = []
+    segs = [(0, 1, 0, n16), (1, 0, 0, n32)]
+    for sid, is16, a0, a1 in segs:
+        for s in range(a0, a1, ce):
+            chunks.append((sid, is16, s, min(a1, s + ce)))
+    arr = np.zeros(len(chunks), dtype=np.dtype([("seg", np.int32), ("is16", np.int32), ("s", np.int64),
+                                                ("e", np.int64)]))
+    for i, c in enumerate(chunks):
+        arr[i] = c
+    dchunks = torch.from_numpy(arr.view(np.uint8)).to(dev)
+    part = torch.empty(len(chunks), device=dev)
+    out = torch.empty(3, device=dev)
+    ops.clip_grad_norm(g16, g32, dchunks, len(chunks), 1.0, part, out)
+    tot_ref = math.sqrt(sum(float(t.float().norm()) ** 2 for t in (g16, g32)))
+    assert abs(out[0].item() - tot_ref) < 1e-3 * tot_ref
+    b16 = torch.empty_like(p16)
+    b32 = torch.empty_like(p32)
+    hyper = torch.tensor([0.01, 0.9, 5e-4, 1.0], device=dev)
+    ops.sgd_step(p16, g16, b16, out, hyper)
+    ops.sgd_step(p32, g32, b32, out, hyper)
+    assert (p16 != rp16.detach()).float().mean().item() < 1e-3
+    torch.testing.assert_close(p32, rp32.detach(), rtol=1e-6, atol=1e-7)
