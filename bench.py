@@ -1,0 +1,230 @@
+"""Benchmark: federated MaPLe client step (ViT-B/16 + text transformer, deep coupled V-L prompts,
+fwd + bwd + clip_grad_norm_ + SGD) on N MI355X, one client per GPU, FedAvg over RCCL at round end.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+One timed "round" = K local steps on every client (one hipGraph replay each, inputs resident in HBM)
+followed by one FedAvg (validity scan + pack + all-reduce + fp16 unpack).  value = images all
+clients processed / max-over-ranks wall time.  Prints ONE JSON line on rank 0.
+
+Workload (BASELINE.json configs): default c4 = per client B=32, K=38 classes (PatternNet shape),
+J=9 prompt depth, the configuration the metric's 1/2/4/8-client scaling is quoted on (configs[3]);
+c2 = configs[1] (J=3, K=10, B=4) is the numerics-gate config, selectable with --config c2.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+from federated_multi_modal_amd import ops  # noqa: E402
+from federated_multi_modal_amd import synthetic as syn  # noqa: E402
+from federated_multi_modal_amd.engine import EngineConfig, MapleEngine  # noqa: E402
+from federated_multi_modal_amd.federated import FedAvgBucket  # noqa: E402
+
+CONFIGS = {
+    # name: (J, K, B, description)
+    "c2": (3, 10, 4, "MaPLe ViT-B/16, 2 prompt tokens, J=3, 10-class synthetic 224x224, batch=4 (configs[1])"),
+    "c3": (9, 10, 4, "EuroSAT-shape 10-class synthetic, J=9, batch=4 per client (configs[2])"),
+    "c4": (9, 38, 32, "PatternNet-shape 38-class synthetic, J=9, batch=32 per client (configs[3])"),
+    "c5": (9, 1000, 32, "ImageNet-shape 1000-class text side, 77-token prompts, J=9, batch=32 (configs[4])"),
+}
+FLOP_PER_IMAGE = 75.04e9   # vision fwd 35.50 + bwd 39.54 GFLOP
+FLOP_PER_CLASS = 12.55e9   # text fwd 5.96 + bwd 6.59 GFLOP
+MFMA_PEAK_F16 = 2.5e15     # MI355X dense fp16 (MI355X_MICROARCH.md: 1024 flop/clk/SIMD x 1024 SIMD x 2.4 GHz)
+HBM_PEAK = 8.0e12
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(J, K, B, budget_s=30.0, seed=0):
+    """The oracle (CPU restatement of the reference, oracle/maple_oracle.py; bit-identical to the
+    reference on the same host) timed on the host cores: forward + backward + clip + SGD of one
+    client step.  Bounded sample: ONE image and ONE class prompt per step (B=1, K=1, same J) --
+    87.6 GFLOP per image against the workload's (B*75.04 + K*12.55)/B GFLOP per image (89.9 at c4),
+    so images/s transfers to the workload's unit; steps are repeated until `budget_s` of CPU time or
+    3 steps.  (The reference's fp16 backward GEMMs run at < 1 GFLOP/s on AMD EPYC hosts: one full
+    c4 step would take many minutes there.)"""
+    from oracle import maple_oracle as O
+    Bs, Ks = 1, 1
+    names = syn.synthetic_classnames(Ks, seed)
+    M = O.build_model(seed, J, names)
+    opt = O.SGDState(lr=0.0026)
+    b = syn.client_batch(seed, 0, 0, Bs, Ks)
+    img, lab = torch.from_numpy(b.images), torch.from_numpy(b.labels)
+    ts = []
+    t_all = time.perf_counter()
+    while len(ts) < 3 and (time.perf_counter() - t_all) < budget_s:
+        t0 = time.perf_counter()
+        O.train_step(M, img, lab, opt)
+        ts.append(time.perf_counter() - t0)
+        log(f"[bench] cpu step {len(ts)}: {ts[-1]:.1f}s")
+    sec = float(np.median(ts[1:])) if len(ts) > 1 else ts[0]
+    return {"value": Bs / sec, "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{len(ts)} step(s) of one client at J={J}, B=1 image, K=1 class prompt "
+                      f"({sec:.2f} s/step{', median after the first' if len(ts) > 1 else ''}), torch-CPU fp16 "
+                      f"oracle, {torch.get_num_threads()} threads; workload per-image work 87.6 vs "
+                      f"{(B * FLOP_PER_IMAGE + K * FLOP_PER_CLASS) / B / 1e9:.1f} GFLOP"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
+    ap.add_argument("--cpu-budget", type=float, default=30.0, help="seconds of CPU-baseline sampling")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--roofline-kernel", default="gemm", choices=["gemm", "attention_fwd"])
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    J, K, B, desc = CONFIGS[args.config]
+    seed = 0
+
+    t0 = time.time()
+    names = syn.synthetic_classnames(K, seed)
+    eng = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed), device=dev)
+    eng.set_lr(0.0026)
+    # two resident synthetic batches per client (client id = rank), alternated step to step
+    batches = []
+    for s in range(2):
+        cb = syn.client_batch(seed, rank, s, B, K)
+        batches.append((torch.from_numpy(cb.images).to(dev), torch.from_numpy(cb.labels).to(dev)))
+    fed = FedAvgBucket(eng)
+    log(f"[bench] engine built in {time.time() - t0:.1f}s (config {args.config}, J={J} K={K} B={B}, world {world})")
+
+    def load(i):
+        img, lab = batches[i % 2]
+        eng.img_in.copy_(img)
+        eng.label_in.copy_(lab)
+
+    if args.no_graph:
+        def step():
+            eng.train_step()
+    else:
+        load(0)
+        eng.train_step()  # first step eager (creates the momentum buffers: first_step flag)
+        graph = eng.capture_train_step()
+
+        def step():
+            graph.replay()
+
+    for i in range(args.warmup):
+        load(i)
+        step()
+    torch.cuda.synchronize()
+    loss_w = eng.loss()  # also the NaN/Inf check of trainers/maple.py:375-376
+
+    # ---------------- timed region: K local steps + one FedAvg round end
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        load(i)
+        step()
+    fed.start()
+    n_valid = fed.finish()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss = eng.loss()
+
+    # ---------------- FedAvg alone (round-end cost), median of 5
+    fts = []
+    for _ in range(5):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        fed.run()
+        torch.cuda.synchronize()
+        fts.append(time.perf_counter() - a)
+    fedavg_ms = 1e3 * float(np.median(fts))
+
+    # ---------------- per-launch roofline of the dominant kernel (eager pass, HIP events on the
+    # launching stream around every launch of that kernel during 2 full steps)
+    probe = ops.KernelProbe(args.roofline_kernel)
+    ops.set_probe(probe)
+    for i in range(2):
+        load(i)
+        eng.train_step()
+    ops.set_probe(None)
+    ps = probe.summary()
+
+    step_flop = B * FLOP_PER_IMAGE + K * FLOP_PER_CLASS
+    value = world * B * args.steps / elapsed
+    if args.roofline_kernel == "gemm":
+        roof = {"bound": "mfma", "achieved": ps["tflops"], "peak": MFMA_PEAK_F16 / 1e12, "unit": "TFLOP/s",
+                "frac": ps["tflops"] * 1e12 / MFMA_PEAK_F16, "traffic": None,
+                "kernel": "gemm_nt_kernel (all projection GEMMs, fwd+bwd)", "launches_per_step": ps["launches"] // 2,
+                "avg_launch_us": ps["avg_us"], "flop_per_launch": ps["flops_per_launch"]}
+    else:
+        roof = {"bound": "mfma", "achieved": ps["tflops"], "peak": MFMA_PEAK_F16 / 1e12, "unit": "TFLOP/s",
+                "frac": ps["tflops"] * 1e12 / MFMA_PEAK_F16, "traffic": None, "kernel": "attention_fwd_kernel",
+                "avg_launch_us": ps["avg_us"], "flop_per_launch": ps["flops_per_launch"]}
+
+    out = {
+        "metric": "images/sec/node (ViT-B/16 MaPLe fwd+bwd)",
+        "value": value,
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp16",
+        "data": "synthetic (portable counter-based PRNG images/labels/token ids; random-init CLIP ViT-B/16 weights)",
+        "config": {"workload": f"{args.config}: {desc}", "clients": world, "batch_per_client": B,
+                   "global_batch": world * B, "classes": K, "prompt_depth": J, "n_ctx": 2,
+                   "parallelism": f"one federated client per GPU x{world}, FedAvg all-reduce per round",
+                   "round": f"{args.steps} local steps + 1 FedAvg", "hipgraph": not args.no_graph},
+        "fedavg_ms": fedavg_ms,
+        "fedavg_valid_clients": n_valid,
+        "model_tflops": world * step_flop * args.steps / elapsed / 1e12,
+        "model_mfma_frac": world * step_flop * args.steps / elapsed / MFMA_PEAK_F16 / world,
+        "loss": loss,
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log(f"[bench] timing the CPU baseline (oracle, {torch.get_num_threads()} threads) ...")
+        out["cpu_baseline"] = cpu_baseline(J, K, B, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

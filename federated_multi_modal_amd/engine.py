@@ -532,13 +532,29 @@ class MapleEngine:
                            self.norm_part, self.clip_out)
         ops.sgd_step(self.flat16, self.gflat16, self.mom16, self.clip_out, self.hyper)
         ops.sgd_step(self.flat32, self.gflat32, self.mom32, self.clip_out, self.hyper)
-        self.hyper[3] = 0.0
+        self.hyper[3:4].zero_()  # a device fill, legal inside graph capture
         self.refresh_transposes(all_layers=False)
 
     def train_step(self):
         self.forward_backward()
         self.optimizer_step()
         self.step_count += 1
+
+    def after_weights_loaded(self):
+        """broadcast_weights (trainers/maple_fed.py:327-339): new weights, SGD momentum dropped."""
+        self.refresh_transposes(all_layers=False)
+        self.reset_momentum()
+
+    def capture_train_step(self, pool=None) -> "torch.cuda.CUDAGraph":
+        """Capture forward + backward + clip + SGD as one hipGraph (static buffers, no host syncs).
+        Replaying it is exactly train_step(); the LR / first-step flag are read from device memory."""
+        first = self.hyper[3].item()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=pool):
+            self.forward_backward()
+            self.optimizer_step()
+        self.hyper[3] = first  # capture does not execute the step
+        return g
 
     # ------------------------------------------------------------------ state
     def loss(self) -> float:

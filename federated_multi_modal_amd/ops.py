@@ -16,6 +16,41 @@ from ._lib import call
 EPI_NONE, EPI_BIAS, EPI_BIAS_RESID, EPI_BIAS_GELU, EPI_DGELU, EPI_F32, EPI_RESID = range(7)
 
 
+class KernelProbe:
+    """Brackets every launch of one kernel family with HIP events on the launching stream (used by
+    bench.py for the per-launch roofline; off by default, never active during graph capture)."""
+
+    def __init__(self, kind: str):
+        self.kind = kind
+        self.records = []  # (start_event, end_event, flops, bytes)
+
+    def around(self, flops: float, nbytes: float):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        self.records.append((s, e, flops, nbytes))
+        return e
+
+    def summary(self):
+        torch.cuda.synchronize()
+        ms = [s.elapsed_time(e) for s, e, _, _ in self.records]
+        n = len(ms)
+        tot_ms = sum(ms)
+        flops = sum(r[2] for r in self.records)
+        nbytes = sum(r[3] for r in self.records)
+        return {"launches": n, "avg_us": 1e3 * tot_ms / max(n, 1), "flops_per_launch": flops / max(n, 1),
+                "bytes_per_launch": nbytes / max(n, 1), "tflops": flops / (tot_ms * 1e-3) / 1e12 if n else 0.0,
+                "gbs": nbytes / (tot_ms * 1e-3) / 1e9 if n else 0.0}
+
+
+_PROBE: Optional[KernelProbe] = None
+
+
+def set_probe(probe: Optional[KernelProbe]):
+    global _PROBE
+    _PROBE = probe
+
+
 def _p(t: Optional[torch.Tensor]):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -38,8 +73,13 @@ def gemm_nt(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NON
         C = torch.empty(M, N, device=A.device, dtype=torch.float32 if epilogue == EPI_F32 else torch.float16)
     aux = aux_in if aux_in is not None else aux_out
     ld_aux = _ld(aux) if aux is not None else 0
+    ev = None
+    if _PROBE is not None and _PROBE.kind == "gemm":
+        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N))
     call("mf_gemm_nt", _p(A), _ld(A), _p(B), _ld(B), _p(C), _ld(C), M, N, K, _p(bias), _p(aux_in), _p(aux_out),
          ld_aux, epilogue, tile, _s())
+    if ev is not None:
+        ev.record()
     return C
 
 
@@ -80,7 +120,13 @@ def attention_fwd(qkv, N, L, H, causal, out=None, lse=None, ld_lse=None):
         ld_lse = L
     if lse is None:
         lse = torch.empty(N * H * ld_lse, device=qkv.device, dtype=torch.float32)
+    ev = None
+    if _PROBE is not None and _PROBE.kind == "attention_fwd":
+        # algorithmic: QK^T + PV = 4 L^2 64 flop per (sequence, head); bytes: Q,K,V read + O write (fp16)
+        ev = _PROBE.around(4.0 * N * H * L * L * 64, 2.0 * 4 * N * L * H * 64)
     call("mf_attention_fwd", _p(qkv), _ld(qkv), _p(out), _ld(out), _p(lse), ld_lse, N, L, H, int(causal), _s())
+    if ev is not None:
+        ev.record()
     return out, lse
 
 

@@ -1,0 +1,189 @@
+"""CPU tier: pin the oracle (oracle/maple_oracle.py) against the golden fixtures generated from the
+reference itself (tests/golden/make_golden.py imports /root/reference's clip/model.py,
+trainers/maple.py and trainers/maple_fed.py), plus the host logic of the product package that
+needs no GPU (synthetic generator, tokenizer, parameter inventory, C-ABI exports)."""
+import ctypes
+import math
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from federated_multi_modal_amd import synthetic as syn
+from oracle import maple_oracle as O
+
+GOLD = Path(__file__).resolve().parent / "golden"
+ROOT = Path(__file__).resolve().parents[1]
+
+
+@pytest.fixture(scope="module")
+def c1():
+    return dict(np.load(GOLD / "c1_maple.npz"))
+
+
+@pytest.fixture(scope="module")
+def c1_oracle(c1):
+    """The oracle's fp16 forward/backward on C1 (J=3, K=10, B=4): ~2 s on 8 CPU cores."""
+    J, K, B, seed = int(c1["J"]), int(c1["K"]), int(c1["B"]), int(c1["seed"])
+    names = syn.synthetic_classnames(K, seed)
+    batch = syn.client_batch(seed, 0, 0, B, K)
+    M = O.build_model(seed, J, names)
+    img = torch.from_numpy(batch.images)
+    lab = torch.from_numpy(batch.labels)
+    with torch.no_grad():
+        logits = O.forward(M, img, train=False)
+    opt = O.SGDState(lr=float(c1["lr"]))
+    before = {k: v.detach().clone() for k, v in M.trainable().items()}
+    loss, grads, total = O.train_step(M, img, lab, opt)
+    deltas = {k: (v.detach().double() - before[k].double()) for k, v in M.trainable().items()}
+    return dict(M=M, logits=logits, loss=loss, grads=grads, total=total, deltas=deltas, labels=batch.labels)
+
+
+def _golden_tensor(g, prefix, name):
+    if f"{prefix}full/{name}" in g:
+        return None, g[f"{prefix}full/{name}"]
+    return g[f"{prefix}idx/{name}"], g[f"{prefix}val/{name}"]
+
+
+def test_golden_inputs_regenerate(c1):
+    """The portable PRNG regenerates the fixture's labels bit-exactly (inputs are not shipped)."""
+    b = syn.client_batch(int(c1["seed"]), 0, 0, int(c1["B"]), int(c1["K"]))
+    assert np.array_equal(b.labels, c1["labels"])
+
+
+def test_oracle_logits_match_reference(c1, c1_oracle):
+    """Oracle eval logits == the reference's (trainers/maple.py:304-346) on the same inputs."""
+    ours = c1_oracle["logits"].float().numpy()
+    ref = c1["logits"].astype(np.float32)
+    assert np.abs(ours - ref).max() <= 1e-3
+    assert np.array_equal(ours.argmax(1), ref.argmax(1))
+    # the fp16 noise floor the 1e-3 gate sits on: fp16-vs-fp64 gap of the reference
+    assert np.abs(ref - c1["logits64"]).max() < 5e-3
+
+
+def test_oracle_loss_and_grads_match_reference(c1, c1_oracle):
+    assert abs(float(c1_oracle["loss"]) - float(c1["loss"])) <= 2e-3
+    assert abs(float(c1_oracle["total"]) - float(c1["total_norm"])) <= 1e-3 * float(c1["total_norm"])
+    grads = c1_oracle["grads"]
+    names = sorted(k[len("grad/norm/"):] for k in c1 if k.startswith("grad/norm/"))
+    assert set(names) == set(grads), set(names) ^ set(grads)
+    for n in names:
+        g = grads[n].double().reshape(-1).numpy()
+        ref_norm = float(c1[f"grad/norm/{n}"])
+        assert abs(np.linalg.norm(g) - ref_norm) <= 1e-2 * ref_norm + 1e-6, n
+        idx, val = _golden_tensor(c1, "grad/", n)
+        got = g if idx is None else g[idx]
+        scale = np.abs(val).max() + 1e-12
+        assert np.abs(got - val).max() <= 2e-2 * scale, n
+
+
+def test_oracle_sgd_deltas_match_reference(c1, c1_oracle):
+    """clip_grad_norm_(1.0) + SGD(momentum .9, wd 5e-4) first step (trainers/maple.py:590-598)."""
+    for k, d in c1_oracle["deltas"].items():
+        if f"delta/norm/{k}" not in c1:
+            continue
+        idx, val = _golden_tensor(c1, "delta/", k)
+        got = d.reshape(-1).numpy()
+        got = got if idx is None else got[idx]
+        scale = np.abs(val).max() + 1e-12
+        assert np.abs(got - val).max() <= 2e-2 * scale + 1e-6, k
+
+
+def test_oracle_fedavg_matches_reference():
+    g = np.load(GOLD / "fedavg.npz")
+    keys = [str(k) for k in g["keys"]]
+    dicts = []
+    for c in range(3):
+        sd = {}
+        for k in keys:
+            dt = torch.float16 if k in ("prompt_learner.ctx",
+                                         "image_encoder.transformer.resblocks.11.attn.in_proj_bias") else torch.float32
+            sd[k] = torch.from_numpy(g[f"in{c}/{k}"]).to(dt)
+        dicts.append(sd)
+    avg = O.safe_average_weights(dicts)
+    for k in keys:
+        assert avg[k].dtype == torch.float16
+        assert np.array_equal(avg[k].float().numpy(), g[f"out/{k}"]), k
+    assert O.check_weights_valid(avg)
+    bad = dict(avg)
+    bad[keys[0]] = bad[keys[0]].clone()
+    bad[keys[0]].view(-1)[0] = float("nan")
+    assert not O.check_weights_valid(bad)
+
+
+# --------------------------------------------------------------------------- host logic (no GPU)
+
+def test_synthetic_generator_is_counter_based():
+    a = syn.normal(7, "x", 100)
+    b = syn.normal(7, "x", 60, start=40)
+    assert np.array_equal(a[40:], b)
+    assert not np.array_equal(syn.normal(8, "x", 10), a[:10])
+    u = syn.uniform(0, "u", 100000)
+    assert 0 <= u.min() and u.max() < 1 and abs(u.mean() - 0.5) < 0.01
+
+
+def test_tokenizer_semantics():
+    t = syn.tokenize(["a photo of a forest.", "a photo of a dense residential."])
+    assert t.shape == (2, 77) and t[0, 0] == syn.SOT_TOKEN
+    eot = t.argmax(-1)
+    assert (t[np.arange(2), eot] == syn.EOT_TOKEN).all()
+    assert eot[1] == eot[0] + 1
+    with pytest.raises(RuntimeError):
+        syn.tokenize(" ".join(["w"] * 80))
+
+
+def test_param_specs_and_trainable_inventory():
+    """The engine's parameter inventory == the reference's CustomCLIP parameters used on the path
+    and the freeze policy of trainers/maple.py:447-479 (counts measured in SURVEY.md §8 a16)."""
+    from federated_multi_modal_amd.engine import EngineConfig, reference_param_specs, _is_trainable
+    for J, n_tr, n_tensors in ((3, 11_879_680, 129), (9, 14_250_496, 147), (11, 15_040_768, 153)):
+        cfg = EngineConfig(batch=4, classnames=["a", "b"], prompt_depth=J)
+        specs = reference_param_specs(cfg)
+        tr = [(n, s) for n, s, _ in specs if _is_trainable(n)]
+        assert len(tr) == n_tensors, (J, len(tr))
+        assert sum(int(np.prod(s)) for _, s in tr) == n_tr, J
+
+
+def test_abi_header_matches_binding():
+    """Every entry point include/mapfed.h declares is bound by _lib.SIGNATURES with the same arity."""
+    from federated_multi_modal_amd import _lib
+    hdr = (ROOT / "include" / "mapfed.h").read_text()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    decls = re.findall(r"\b(?:int|const char\*)\s+(mf_\w+)\s*\(([^)]*)\)\s*;", hdr)
+    assert len(decls) >= 25
+    for name, args in decls:
+        assert name in _lib.exported_symbols(), name
+        if name == "mf_last_error":
+            continue
+        n = 0 if args.strip() in ("", "void") else len(args.split(","))
+        assert len(_lib.SIGNATURES[name]) == n, (name, n, len(_lib.SIGNATURES[name]))
+
+
+def test_library_loads_and_exports_every_symbol():
+    """libmapfed.so (built by __graft_entry__.build()) loads without a GPU and exports the ABI."""
+    from federated_multi_modal_amd import _lib
+    if not _lib.LIB_PATH.exists():
+        import __graft_entry__
+        __graft_entry__.build()
+    h = ctypes.CDLL(str(_lib.LIB_PATH))
+    for name in _lib.exported_symbols():
+        assert hasattr(h, name), name
+    h.mf_abi_version.restype = ctypes.c_int
+    assert h.mf_abi_version() == 1
+    assert _lib.call("mf_optim_chunk_elems") > 0
+    # argument validation runs on the host, before any launch
+    rc = h.mf_gemm_nt(None, 64, None, 64, None, 64, 8, 8, 63, None, None, None, 0, 0, 0, None)
+    assert rc != 0
+    h.mf_last_error.restype = ctypes.c_char_p
+    assert b"multiple of 64" in h.mf_last_error()
+
+
+def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
+    from federated_multi_modal_amd import _lib
+    monkeypatch.setattr(_lib, "_LIB", None)
+    monkeypatch.setenv("MAPFED_LIB", str(tmp_path / "missing.so"))
+    with pytest.raises(_lib.MapfedError):
+        _lib.lib()
+    monkeypatch.setattr(_lib, "_LIB", None)
