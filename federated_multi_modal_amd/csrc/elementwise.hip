@@ -139,25 +139,34 @@ __global__ void transpose_kernel(const f16* __restrict__ in, int64_t ld_in, f16*
 }
 
 // ---------------------------------------------------------------- column sums (bias grads)
-constexpr int CS_ROWS = 256;
-__global__ void colsum_part_kernel(const f16* __restrict__ in, int64_t ld, int R, int C, float* __restrict__ part) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const int r0 = blockIdx.y * CS_ROWS;
-  const int r1 = min(R, r0 + CS_ROWS);
-  float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += (float)in[(int64_t)r * ld + c];
-  part[(int64_t)blockIdx.y * C + c] = s;
-}
-__global__ void colsum_final_kernel(const float* __restrict__ part, int nb, int C, void* out, int out_f16) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[(int64_t)b * C + c];
-  if (out_f16)
-    ((f16*)out)[c] = (f16)s;
-  else
-    ((float*)out)[c] = s;
+// part[chunk][c] = sum of rows [64*chunk, 64*chunk+64) of column c: a block of 256 threads covers
+// 256 columns (4 per lane, 8-byte loads) x 64 rows (16 per wave); then col_reduce_kernel.
+constexpr int CS_ROWS = 64;
+__global__ __launch_bounds__(256) void colsum_part_kernel(const f16* __restrict__ in, int64_t ld, int R, int C,
+                                                          float* __restrict__ part) {
+  __shared__ f32x4 red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + lane * 4;
+  const int r0 = blockIdx.y * CS_ROWS + w * 16;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+#pragma unroll 4
+    for (int r = r0; r < min(R, r0 + 16); ++r) {
+      f16x4 v = *(const f16x4*)(in + (int64_t)r * ld + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[e] += (float)v[e];
+    }
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    f32x4 t = red[0][lane];
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[e] += red[k][lane][e];
+    *(f32x4*)(part + (int64_t)blockIdx.y * C + c) = t;
+  }
 }
 
 // ---------------------------------------------------------------- small linears (M rows <= 16)
@@ -174,19 +183,37 @@ __global__ void small_linear_fwd_kernel(const T* __restrict__ X, const T* __rest
   s = wave_sum(s);
   if (lane == 0) Y[(int64_t)m * O + o] = (T)(s + (b ? (float)b[o] : 0.f));
 }
-// dX[m,i] (=|+=) sum_o dY[m,o] W[o,i]   ; fp16 accumulate rounds the new term once then adds
+// dX[m,i] (=|+=) sum_o dY[m,o] W[o,i]   ; fp16 accumulate rounds the new term once then adds.
+// grid (I/64, M), 1024 threads: lane -> column i, 16 wave groups split the o range (fixed order
+// LDS reduction), so the O-long dot product is 16-way parallel instead of one serial chain.
 template <typename T>
-__global__ void small_linear_bwd_dx_kernel(const T* __restrict__ dY, const T* __restrict__ W, T* __restrict__ dX,
-                                           int M, int I, int O, int accumulate) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= M * I) return;
-  const int m = t / I, i = t % I;
-  float s = 0.f;
-  for (int o = 0; o < O; ++o) s += (float)dY[(int64_t)m * O + o] * (float)W[(int64_t)o * I + i];
-  if (accumulate)
-    dX[t] = (T)((float)dX[t] + (float)(T)s);
-  else
-    dX[t] = (T)s;
+__global__ __launch_bounds__(1024) void small_linear_bwd_dx_kernel(const T* __restrict__ dY,
+                                                                   const T* __restrict__ W, T* __restrict__ dX,
+                                                                   int M, int I, int O, int accumulate) {
+  __shared__ float red[16][65];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane, m = blockIdx.y;
+  float s0 = 0.f, s1 = 0.f;
+  if (i < I) {
+    int o = g;
+    for (; o + 16 < O; o += 32) {
+      s0 += (float)dY[(int64_t)m * O + o] * (float)W[(int64_t)o * I + i];
+      s1 += (float)dY[(int64_t)m * O + o + 16] * (float)W[(int64_t)(o + 16) * I + i];
+    }
+    for (; o < O; o += 16) s0 += (float)dY[(int64_t)m * O + o] * (float)W[(int64_t)o * I + i];
+  }
+  red[g][lane] = s0 + s1;
+  __syncthreads();
+  if (g == 0 && i < I) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][lane];
+    const int64_t t = (int64_t)m * I + i;
+    if (accumulate)
+      dX[t] = (T)((float)dX[t] + (float)(T)s);
+    else
+      dX[t] = (T)s;
+  }
 }
 // dW[o,i] = sum_m dY[m,o] X[m,i] ; db[o] = sum_m dY[m,o]
 template <typename T>
@@ -285,10 +312,14 @@ extern "C" int mf_colsum_f16(const void* in, int64_t ld, int R, int C, void* out
   if (R <= 0 || C <= 0) return 0;
   const int nb = mf_colsum_blocks(R);
   hipStream_t st = (hipStream_t)stream;
+  if (C % 4 || ld % 4) return mf_set_error("mf_colsum_f16: C and ld must be multiples of 4", -1);
   dim3 grid((C + 255) / 256, nb);
   colsum_part_kernel<<<grid, 256, 0, st>>>((const f16*)in, ld, R, C, workspace);
   MF_CHECK_LAUNCH();
-  colsum_final_kernel<<<(C + 255) / 256, 256, 0, st>>>(workspace, nb, C, out, out_f16);
+  if (out_f16)
+    col_reduce_kernel<true><<<dim3((C + 63) / 64, 1), 1024, 0, st>>>(workspace, workspace, nb, C, C, out, out, 0);
+  else
+    col_reduce_kernel<false><<<dim3((C + 63) / 64, 1), 1024, 0, st>>>(workspace, workspace, nb, C, C, out, out, 0);
   MF_CHECK_LAUNCH();
   return 0;
 }
@@ -314,15 +345,15 @@ extern "C" int mf_small_linear_bwd(const void* dY, const void* X, const void* W,
   hipStream_t st = (hipStream_t)stream;
   if (is_f16) {
     if (dX)
-      small_linear_bwd_dx_kernel<f16><<<nblk((int64_t)M * I), 256, 0, st>>>((const f16*)dY, (const f16*)W, (f16*)dX,
-                                                                            M, I, O, accumulate_dx);
+      small_linear_bwd_dx_kernel<f16><<<dim3((I + 63) / 64, M), 1024, 0, st>>>((const f16*)dY, (const f16*)W,
+                                                                                (f16*)dX, M, I, O, accumulate_dx);
     if (dW)
       small_linear_bwd_dw_kernel<f16><<<nblk((int64_t)O * I), 256, 0, st>>>((const f16*)dY, (const f16*)X, (f16*)dW,
                                                                             (f16*)db, M, I, O);
   } else {
     if (dX)
-      small_linear_bwd_dx_kernel<float><<<nblk((int64_t)M * I), 256, 0, st>>>((const float*)dY, (const float*)W,
-                                                                              (float*)dX, M, I, O, accumulate_dx);
+      small_linear_bwd_dx_kernel<float><<<dim3((I + 63) / 64, M), 1024, 0, st>>>(
+          (const float*)dY, (const float*)W, (float*)dX, M, I, O, accumulate_dx);
     if (dW)
       small_linear_bwd_dw_kernel<float><<<nblk((int64_t)O * I), 256, 0, st>>>((const float*)dY, (const float*)X,
                                                                               (float*)dW, (float*)db, M, I, O);

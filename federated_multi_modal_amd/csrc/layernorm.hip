@@ -14,7 +14,7 @@
 namespace {
 
 constexpr int LN_WAVES = 4;
-constexpr int LN_ROWS_PER_BLOCK = 32;
+constexpr int LN_ROWS_PER_BLOCK = 16;
 
 // y = ((x*rstd) + (-rstd*mean)) * gamma + beta, the operation order of torch's CPU kernel
 template <int D>
@@ -168,16 +168,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const f16* __restrict__ dy,
   }
 }
 
-// out[col] (=|+=) sum_b part[b][col], fixed order -> deterministic
-__global__ void col_reduce_f32_kernel(const float* __restrict__ part, int nblk, int D, float* __restrict__ out,
-                                      int accumulate) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= D) return;
-  float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * D + col];
-  out[col] = accumulate ? out[col] + s : s;
-}
-
 }  // namespace
 
 extern "C" int mf_layernorm_fwd(const void* x, int64_t ldx, const int* row_index, const float* gamma,
@@ -215,8 +205,8 @@ extern "C" int mf_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int
     ln_bwd_kernel<512><<<nblk, 256, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, row_index, gamma, mean, rstd,
                                              (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows);
   MF_CHECK_LAUNCH();
-  col_reduce_f32_kernel<<<(D + 255) / 256, 256, 0, st>>>(dg_part, nblk, D, dgamma, accumulate);
-  col_reduce_f32_kernel<<<(D + 255) / 256, 256, 0, st>>>(db_part, nblk, D, dbeta, accumulate);
+  col_reduce_kernel<false><<<dim3((D + 63) / 64, 2), 1024, 0, st>>>(dg_part, db_part, nblk, D, D, dgamma, dbeta,
+                                                                    accumulate);
   MF_CHECK_LAUNCH();
   return 0;
 }

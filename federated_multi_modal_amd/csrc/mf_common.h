@@ -52,6 +52,49 @@ MF_DEV float quick_gelu16_bwd(float dg, float f) {
   return r16(da + db);
 }
 
+// Deterministic column reduction of `nblk` partial rows: out[c] (=|+=) sum_b part[b*ld + c].
+// One 1024-thread block per 64 columns: 16 row groups x 64 lanes, each lane summing its group's rows
+// with 4 independent loads in flight, then a fixed-order LDS reduction over the 16 groups (the same
+// order on every launch -> bitwise reproducible).  Up to two (part, out) pairs per launch
+// (blockIdx.y selects the pair: LayerNorm dgamma and dbeta in one launch).
+namespace {
+template <bool OUT16>
+__global__ __launch_bounds__(1024) void col_reduce_kernel(const float* __restrict__ part0,
+                                                          const float* __restrict__ part1, int nblk, int C,
+                                                          int64_t ld, void* out0, void* out1, int accumulate) {
+  __shared__ float red[16][65];
+  const float* part = blockIdx.y ? part1 : part0;
+  void* out = blockIdx.y ? out1 : out0;
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < C) {
+    int b = g;
+    for (; b + 48 < nblk; b += 64) {
+      s0 += part[(int64_t)b * ld + c];
+      s1 += part[(int64_t)(b + 16) * ld + c];
+      s2 += part[(int64_t)(b + 32) * ld + c];
+      s3 += part[(int64_t)(b + 48) * ld + c];
+    }
+    for (; b < nblk; b += 16) s0 += part[(int64_t)b * ld + c];
+  }
+  red[g][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (g == 0 && c < C) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][lane];
+    if (OUT16) {
+      f16* o = (f16*)out + c;
+      *o = accumulate ? (f16)((float)*o + s) : (f16)s;
+    } else {
+      float* o = (float*)out + c;
+      *o = accumulate ? *o + s : s;
+    }
+  }
+}
+}  // namespace
+
 #define MF_CHECK_LAUNCH()                                                     \
   do {                                                                        \
     hipError_t _e = hipGetLastError();                                        \

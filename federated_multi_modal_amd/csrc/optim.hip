@@ -47,32 +47,65 @@ __global__ void sumsq_chunks_kernel(const f16* __restrict__ g16, const float* __
   if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-// One block: per-segment norms (chunks of a segment are consecutive), total, clip coefficient.
+// One block of 1024 threads: per-segment norms from the per-chunk partial sums (the chunks of a
+// segment are consecutive), total norm, clip coefficient.  The chunk list is walked in tiles of 1024
+// with a segmented inclusive scan (Hillis-Steele in LDS, fixed order -> deterministic); the last
+// chunk of each segment yields that segment's sum of squares (plus the carry of a segment that
+// started in an earlier tile).  torch.nn.utils.clip_grad_norm_: per-tensor norms in the grad's dtype
+// (fp16 tensors round their norm to fp16), total = ||(norm_t)_t||_2 in fp32,
+// coef = clamp(max_norm / (total + 1e-6), max 1).
 // out[0] = total norm, out[1] = clip coef, out[2] = 1 if total is finite else 0
-__global__ void clip_coef_kernel(const float* __restrict__ part, const Chunk* __restrict__ chunks, int nchunks,
-                                 float max_norm, float* __restrict__ out) {
-  __shared__ float red[256];
+__global__ __launch_bounds__(1024) void clip_coef_kernel(const float* __restrict__ part,
+                                                         const Chunk* __restrict__ chunks, int nchunks,
+                                                         float max_norm, float* __restrict__ out) {
+  __shared__ float sv[1024];
+  __shared__ int sseg[1024];
+  __shared__ float red[16];
+  __shared__ float carry_val;
+  __shared__ int carry_seg;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    carry_val = 0.f;
+    carry_seg = -1;
+  }
   float acc = 0.f;
-  // every thread walks the chunk list; thread t owns the segments whose index % 256 == t
-  int c = 0;
-  while (c < nchunks) {
-    const int seg = chunks[c].seg;
-    const int is16 = chunks[c].is16;
-    float ss = 0.f;
-    int cc = c;
-    while (cc < nchunks && chunks[cc].seg == seg) ss += part[cc++];
-    if ((seg & 255) == (int)threadIdx.x) {
+  for (int base = 0; base < nchunks; base += 1024) {
+    const int c = base + t;
+    const int seg = c < nchunks ? chunks[c].seg : -1;
+    float v = c < nchunks ? part[c] : 0.f;
+    sseg[t] = seg;
+    sv[t] = v;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      float add = 0.f;
+      if (t >= off && sseg[t - off] == seg) add = sv[t - off];
+      __syncthreads();
+      v += add;
+      sv[t] = v;
+      __syncthreads();
+    }
+    const bool last = c < nchunks && (c == nchunks - 1 || chunks[c + 1].seg != seg);
+    if (last) {
+      float ss = v;
+      if (seg == carry_seg && sseg[0] == seg) ss += carry_val;  // segment began in an earlier tile
       float nrm = sqrtf(ss);
-      if (is16) nrm = r16(nrm);
+      if (chunks[c].is16) nrm = r16(nrm);
       acc += nrm * nrm;
     }
-    c = cc;
+    __syncthreads();
+    if (t == 1023) {
+      const float prev = (seg == carry_seg && sseg[0] == seg) ? carry_val : 0.f;
+      carry_val = v + prev;
+      carry_seg = seg;
+    }
+    __syncthreads();
   }
-  red[threadIdx.x] = acc;
+  acc = wave_sum(acc);
+  if ((t & 63) == 0) red[t >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     float tot = 0.f;
-    for (int i = 0; i < 256; ++i) tot += red[i];
+    for (int i = 0; i < 16; ++i) tot += red[i];
     const float total = sqrtf(tot);
     float coef = max_norm / (total + 1e-6f);
     coef = coef > 1.f ? 1.f : coef;
@@ -152,7 +185,7 @@ extern "C" int mf_clip_grad_norm(const void* g16, const float* g32, const void* 
   if (nchunks <= 0) return 0;
   sumsq_chunks_kernel<<<nchunks, 256, 0, st>>>((const f16*)g16, g32, (const Chunk*)chunks, part);
   MF_CHECK_LAUNCH();
-  clip_coef_kernel<<<1, 256, 0, st>>>(part, (const Chunk*)chunks, nchunks, max_norm, out);
+  clip_coef_kernel<<<1, 1024, 0, st>>>(part, (const Chunk*)chunks, nchunks, max_norm, out);
   MF_CHECK_LAUNCH();
   return 0;
 }

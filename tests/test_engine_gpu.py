@@ -99,18 +99,20 @@ def test_c1_grads(c1, c1_engine):
 
 def test_c1_sgd_deltas(c1, c1_engine):
     """fp32 params: relative L2 error of the update <= 5 %.  fp16 params store p - lr*buf rounded to
-    fp16, so their update is quantised to ulps of p: each element may differ by at most one fp16
-    ulp of p (a rounding flip), in at most 25 % of elements."""
+    fp16, so their update is quantised to ulps of p: per element the difference may be one fp16 ulp
+    of p (a rounding flip) plus 10 % of the update (the gradient's own error), and over the tensor
+    ||diff|| <= 5 % ||update|| + half the rms ulp."""
     worst = 0.0
     for n, d in c1_engine["deltas"].items():
         if f"delta/norm/{n}" not in c1:
             continue
         ours, ref = _sel(c1, "delta/", n, d)
+        diff = np.abs(ours - ref)
         if c1_engine["dtypes"][n] == torch.float16:
             p0, _ = _sel(c1, "delta/", n, c1_engine["before"][n])
             u = np.exp2(np.floor(np.log2(np.maximum(np.abs(p0), 2.0 ** -14))) - 10)
-            diff = np.abs(ours - ref) / u
-            assert diff.max() <= 1.0 + 1e-6 and (diff > 0.5).mean() <= 0.25, (n, diff.max(), (diff > 0.5).mean())
+            assert (diff <= u + 0.1 * np.abs(ref) + 1e-12).all(), (n, (diff / u).max())
+            assert np.linalg.norm(diff) <= 0.05 * np.linalg.norm(ref) + 0.5 * np.linalg.norm(u), n
             continue
         if np.linalg.norm(ref) == 0:
             continue
