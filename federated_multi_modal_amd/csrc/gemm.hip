@@ -44,22 +44,41 @@ constexpr int BK = 64;
 
 MF_DEV int swz(int row, int chunk) { return chunk ^ (row & 7); }
 
-template <int BM, int BN, int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int A_CH = BM * 8 / 256;  // 16-B chunks per thread per A tile
-  constexpr int B_CH = BN * 8 / 256;
-  __shared__ __attribute__((aligned(16))) f16 lds[2 * (BM + BN) * BK];
-  f16* ldsA = lds;
-  f16* ldsB = lds + 2 * BM * BK;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// s_waitcnt vmcnt(n) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt[5:4]<<14)
+template <int N>
+MF_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// Tile BM x BN, (WM x WN) waves each owning a (BM/WM) x (BN/WN) block of 16x16 MFMA tiles, BK = 64.
+// Operands go HBM -> LDS by global_load_lds (16 B per lane, no VGPR round trip): each wave
+// instruction fills 8 rows x 128 B of the [rows][64] fp16 image; the 16-B-chunk XOR swizzle
+// (chunk ^ (row & 7)) is applied to the per-lane SOURCE address (the LDS side is lane-linear), so
+// the ds_read_b128 fragment reads stay conflict-free.  Two LDS buffers: the loads of K-step t+1
+// are issued before the fragment reads + MFMAs of step t and drained by one vmcnt(0) + barrier
+// per step (cdna_hip_programming.md §5.5 T3/T4 minimum 2-phase form).
+template <int BM, int BN, int WM, int WN, int S, int EPI, bool PRIO = false>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g) {
+  constexpr int NW = WM * WN;
+  constexpr int NT = NW * 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;  // per-wave tile
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int A_INS = BM / 8 / NW;  // glds wave-instructions per stage per wave
+  constexpr int B_INS = BN / 8 / NW;
+  static_assert(A_INS * 8 * NW == BM && B_INS * 8 * NW == BN, "tile / wave split");
+  constexpr int STAGE = (BM + BN) * BK;  // fp16 elements per stage
+  __shared__ __attribute__((aligned(1024))) f16 lds[S * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wave_m = wid >> 1, wave_n = wid & 1;
+  const int wave_m = wid / WN, wave_n = wid % WN;
 
-  // XCD-aware bijective remap (cdna_hip_programming.md §5 'XCD swizzle must be bijective')
+  // XCD-aware bijective remap (cdna_hip_programming.md §5 'XCD swizzle must be bijective'):
+  // consecutive tile ids (same A row panel) land on one XCD's L2
   const int tiles_n = (g.N + BN - 1) / BN;
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
@@ -68,44 +87,34 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
   const int m0 = (wgid / tiles_n) * BM;
   const int n0 = (wgid % tiles_n) * BN;
 
-  // staging coordinates
-  const int st_c = tid & 7;
-  const int st_r = tid >> 3;  // 0..31
-  const f16* a_src[A_CH];
-  const f16* b_src[B_CH];
+  // per-lane glds sources: instruction i of this wave covers tile rows (wid*A_INS + i)*8 + lane/8
+  const int lrow = lane >> 3;
+  const int lchunk = (lane & 7) ^ lrow;  // pre-swizzled source chunk (row & 7 == lrow)
+  const f16* a_src[A_INS];
+  const f16* b_src[B_INS];
 #pragma unroll
-  for (int i = 0; i < A_CH; ++i) {
-    int row = m0 + st_r + 32 * i;
+  for (int i = 0; i < A_INS; ++i) {
+    int row = m0 + (wid * A_INS + i) * 8 + lrow;
     row = row < g.M ? row : g.M - 1;
-    a_src[i] = g.A + (int64_t)row * g.lda + st_c * 8;
+    a_src[i] = g.A + (int64_t)row * g.lda + lchunk * 8;
   }
 #pragma unroll
-  for (int i = 0; i < B_CH; ++i) {
-    int row = n0 + st_r + 32 * i;
+  for (int i = 0; i < B_INS; ++i) {
+    int row = n0 + (wid * B_INS + i) * 8 + lrow;
     row = row < g.N ? row : g.N - 1;
-    b_src[i] = g.B + (int64_t)row * g.ldb + st_c * 8;
+    b_src[i] = g.B + (int64_t)row * g.ldb + lchunk * 8;
   }
-  f16x8 ra[A_CH], rb[B_CH];
-
-  auto load_regs = [&](int k0) {
+  auto stage = [&](int buf, int k0) {
+    f16* la = lds + buf * STAGE;
+    f16* lb = la + BM * BK;
 #pragma unroll
-    for (int i = 0; i < A_CH; ++i) ra[i] = *(const f16x8*)(a_src[i] + k0);
+    for (int i = 0; i < A_INS; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + k0),
+                                       (lds_ptr_t)(la + (wid * A_INS + i) * 8 * BK), 16, 0, 0);
 #pragma unroll
-    for (int i = 0; i < B_CH; ++i) rb[i] = *(const f16x8*)(b_src[i] + k0);
-  };
-  auto write_lds = [&](int buf) {
-    f16* la = ldsA + buf * BM * BK;
-    f16* lb = ldsB + buf * BN * BK;
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      int row = st_r + 32 * i;
-      *(f16x8*)(la + row * BK + swz(row, st_c) * 8) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      int row = st_r + 32 * i;
-      *(f16x8*)(lb + row * BK + swz(row, st_c) * 8) = rb[i];
-    }
+    for (int i = 0; i < B_INS; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + k0),
+                                       (lds_ptr_t)(lb + (wid * B_INS + i) * 8 * BK), 16, 0, 0);
   };
 
   f32x4 acc[TM][TN];
@@ -115,47 +124,61 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nk = g.K / BK;
-  load_regs(0);
-  write_lds(0);
-  __syncthreads();
+  // prologue: S-1 stages in flight
+#pragma unroll
+  for (int p = 0; p < S - 1; ++p)
+    if (p < nk) stage(p, p * BK);
 
   const int fr = lane & 15, fg = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_regs((kt + 1) * BK);
-    const f16* la = ldsA + cur * BM * BK;
-    const f16* lb = ldsB + cur * BN * BK;
+    // stage kt landed (this wave's DMA: leave the younger stages in flight), then one barrier:
+    // every wave's DMA for kt is visible and every wave is done reading stage kt-1's buffer
+    const int younger = min(S - 2, nk - 1 - kt);
+    if constexpr (S >= 3) {
+      if (younger >= 2) wait_vmcnt<2 * (A_INS + B_INS)>();
+      else if (younger == 1) wait_vmcnt<A_INS + B_INS>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kt + S - 1 < nk) stage((kt + S - 1) % S, (kt + S - 1) * BK);
+    const f16* la = lds + (kt % S) * STAGE;
+    const f16* lb = la + BM * BK;
+    // fragments of sub-step 1 are read while the MFMAs of sub-step 0 run (register double buffer)
+    f16x8 af[2][TM], bf[2][TN];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      f16x8 af[TM], bf[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        int row = wave_m * WM + i * 16 + fr;
-        af[i] = *(const f16x8*)(la + row * BK + swz(row, 4 * s + fg) * 8);
+        const int row = wave_m * WTM + i * 16 + fr;
+        af[s][i] = *(const f16x8*)(la + row * BK + swz(row, 4 * s + fg) * 8);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        int row = wave_n * WN + j * 16 + fr;
-        bf[j] = *(const f16x8*)(lb + row * BK + swz(row, 4 * s + fg) * 8);
+        const int row = wave_n * WTN + j * 16 + fr;
+        bf[s][j] = *(const f16x8*)(lb + row * BK + swz(row, 4 * s + fg) * 8);
       }
+    }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
-    }
-    if (kt + 1 < nk) write_lds(cur ^ 1);
-    __syncthreads();
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[s][j], af[s][i], acc[i][j], 0, 0, 0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   }
 
   // epilogue: lane holds C[m = .. + fr][n = .. + 4*fg + e], e = 0..3
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wave_m * WM + i * 16 + fr;
+    const int m = m0 + wave_m * WTM + i * 16 + fr;
     if (m >= g.M) continue;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wave_n * WN + j * 16 + 4 * fg;
+      const int n = n0 + wave_n * WTN + j * 16 + 4 * fg;
       if (n >= g.N) continue;
       f32x4 v = acc[i][j];
       if constexpr (EPI == EPI_F32) {
@@ -200,18 +223,18 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WM, int WN, int S>
 int launch_tile(const GemmArgs& a, int epi, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  dim3 grid(tiles), block(256);
+  dim3 grid(tiles), block(WM * WN * 64);
   switch (epi) {
-    case EPI_NONE: gemm_nt_kernel<BM, BN, EPI_NONE><<<grid, block, 0, st>>>(a); break;
-    case EPI_BIAS: gemm_nt_kernel<BM, BN, EPI_BIAS><<<grid, block, 0, st>>>(a); break;
-    case EPI_BIAS_RESID: gemm_nt_kernel<BM, BN, EPI_BIAS_RESID><<<grid, block, 0, st>>>(a); break;
-    case EPI_BIAS_GELU: gemm_nt_kernel<BM, BN, EPI_BIAS_GELU><<<grid, block, 0, st>>>(a); break;
-    case EPI_DGELU: gemm_nt_kernel<BM, BN, EPI_DGELU><<<grid, block, 0, st>>>(a); break;
-    case EPI_F32: gemm_nt_kernel<BM, BN, EPI_F32><<<grid, block, 0, st>>>(a); break;
-    case EPI_RESID: gemm_nt_kernel<BM, BN, EPI_RESID><<<grid, block, 0, st>>>(a); break;
+    case EPI_NONE: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_NONE><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_BIAS><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_RESID: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_BIAS_RESID><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_GELU: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_BIAS_GELU><<<grid, block, 0, st>>>(a); break;
+    case EPI_DGELU: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_DGELU><<<grid, block, 0, st>>>(a); break;
+    case EPI_F32: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_F32><<<grid, block, 0, st>>>(a); break;
+    case EPI_RESID: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_RESID><<<grid, block, 0, st>>>(a); break;
     default: return mf_set_error("mf_gemm_nt: bad epilogue", -2);
   }
   MF_CHECK_LAUNCH();
@@ -236,12 +259,23 @@ extern "C" int mf_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb
   hipStream_t st = (hipStream_t)stream;
   if (tile == 0) {  // heuristic: fill the 256 CUs
     int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
-    tile = t128 >= 512 ? 1 : (t128 >= 128 ? 2 : 3);
+    tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);  // measured: tests/diagnostics/gemm_bench.py
   }
   switch (tile) {
-    case 1: return launch_tile<128, 128>(a, epilogue, st);
-    case 2: return launch_tile<128, 64>(a, epilogue, st);
-    case 3: return launch_tile<64, 64>(a, epilogue, st);
+    case 1: return launch_tile<128, 128, 2, 2, 2>(a, epilogue, st);
+    case 2: return launch_tile<128, 64, 2, 2, 2>(a, epilogue, st);
+    case 3: return launch_tile<64, 64, 2, 2, 2>(a, epilogue, st);
+    case 4: return launch_tile<256, 128, 4, 2, 2>(a, epilogue, st);
+    case 5: return launch_tile<256, 128, 4, 2, 3>(a, epilogue, st);
+    case 6: return launch_tile<128, 128, 2, 2, 3>(a, epilogue, st);
+    case 7: return launch_tile<128, 64, 2, 2, 3>(a, epilogue, st);
+    case 8: return launch_tile<128, 256, 2, 4, 3>(a, epilogue, st);
+    case 9: return launch_tile<256, 256, 2, 4, 2>(a, epilogue, st);
+    case 10: return launch_tile<256, 128, 2, 2, 3>(a, epilogue, st);
+    case 11: return launch_tile<128, 128, 2, 2, 4>(a, epilogue, st);
+    case 12: return launch_tile<256, 128, 2, 2, 2>(a, epilogue, st);
+    case 13: return launch_tile<128, 256, 2, 2, 3>(a, epilogue, st);
+    case 14: return launch_tile<128, 64, 2, 2, 4>(a, epilogue, st);
     default: return mf_set_error("mf_gemm_nt: bad tile id", -2);
   }
 }

@@ -265,6 +265,7 @@ class MapleEngine:
         self.txt = _Tower(self, "text_encoder", self.K, d.context_length, d.text_width, d.text_heads, d.text_layers,
                           True, 1)
         self._build_io()
+        self.side = torch.cuda.Stream(device=self.device)
         self.step_count = 0
         self.hyper = torch.tensor([0.0, cfg.momentum, cfg.weight_decay, 1.0], device=self.device, dtype=F32)
         self.momentum_initialised = False
@@ -399,6 +400,7 @@ class MapleEngine:
         self.dimg, self.dtxt = e(B, E), e(K, E)
         self.d_vis_post, self.d_txt_final = e(B, dv), e(K, dt)
         self.dXpre = e(B * self.Lv, dv)
+        self.ln_ws_text = e(ops.layernorm_ws_floats(K, dt), dt_=F32)  # text tower runs on the side stream
         self.ln_ws_small = e(max(ops.layernorm_ws_floats(max(B, K), dv), ops.layernorm_ws_floats(B * self.Lv, dv)),
                              dt_=F32)
 
@@ -472,10 +474,17 @@ class MapleEngine:
         ops.gemm_nt(self.vis_post, self.projT, self.img_feat, epilogue=ops.EPI_NONE)
 
     def forward(self):
-        """CustomCLIP.forward up to the logits (eval path, trainers/maple.py:304-346)."""
+        """CustomCLIP.forward up to the logits (eval path, trainers/maple.py:304-346).  The text and
+        vision towers are independent until the head: the text tower runs on a side stream, forked
+        from and joined back into the current stream (also inside a captured hipGraph), so its
+        smaller kernels fill the CUs the vision GEMMs leave idle."""
         self._prompt_learner_fwd()
-        self._text_forward()
+        main = torch.cuda.current_stream(self.device)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            self._text_forward()
         self._vision_forward()
+        main.wait_stream(self.side)
         ops.clip_head_fwd(self.img_feat, self.txt_feat, self.P["logit_scale"], self.img_n, self.txt_n, self.norms,
                           self.mm, self.logits)
         return self.logits
@@ -487,7 +496,7 @@ class MapleEngine:
         ops.gemm_nt(self.dtxt, P["text_encoder.text_projection"], self.d_txt_final, epilogue=ops.EPI_NONE)
         t.dX.zero_()
         ops.layernorm_bwd(self.d_txt_final, t.X[-1], P["text_encoder.ln_final.weight"], self.fin_mean, self.fin_rstd,
-                          t.dX, G["text_encoder.ln_final.weight"], G["text_encoder.ln_final.bias"], self.ln_ws_small,
+                          t.dX, G["text_encoder.ln_final.weight"], G["text_encoder.ln_final.bias"], self.ln_ws_text,
                           row_index=self.eot_rows)
         t.backward(self.J - 1, self.g_txt_deep)
         # d ctx (text path): sum over classes of the rows 1..n_ctx of d prompts (fp16 result)
@@ -514,8 +523,12 @@ class MapleEngine:
         ops.clip_loss_fwd_bwd(self.img_feat, self.txt_feat, self.img_n, self.txt_n, self.norms, self.logits,
                               self.label_in, self.P["logit_scale"], self.dmm, self.cos_ws, self.loss_out,
                               self.dimg_n, self.dtxt_n, self.dimg, self.dtxt)
-        self._text_backward()
+        main = torch.cuda.current_stream(self.device)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            self._text_backward()
         self._vision_backward()
+        main.wait_stream(self.side)
         self._prompt_learner_bwd()
 
     # ------------------------------------------------------------------ optimizer
