@@ -147,7 +147,7 @@ def main():
         load(i)
         step()
     fed.start()
-    n_valid = fed.finish()
+    fed.finish()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     if world > 1:
@@ -171,12 +171,15 @@ def main():
 
     # ---------------- per-launch roofline of the dominant kernel (eager pass, HIP events on the
     # launching stream around every launch of that kernel during 2 full steps)
+    # (towers serialised on one stream here so that no other kernel runs inside a probed launch)
     probe = ops.KernelProbe(args.roofline_kernel)
+    eng.overlap_towers = False
     ops.set_probe(probe)
     for i in range(2):
         load(i)
         eng.train_step()
     ops.set_probe(None)
+    eng.overlap_towers = True
     ps = probe.summary()
 
     step_flop = B * FLOP_PER_IMAGE + K * FLOP_PER_CLASS
@@ -209,7 +212,7 @@ def main():
                    "parallelism": f"one federated client per GPU x{world}, FedAvg all-reduce per round",
                    "round": f"{args.steps} local steps + 1 FedAvg", "hipgraph": not args.no_graph},
         "fedavg_ms": fedavg_ms,
-        "fedavg_valid_clients": n_valid,
+        "fedavg_valid_clients": fed.n_valid(),
         "model_tflops": world * step_flop * args.steps / elapsed / 1e12,
         "model_mfma_frac": world * step_flop * args.steps / elapsed / MFMA_PEAK_F16 / world,
         "loss": loss,

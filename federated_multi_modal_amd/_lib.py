@@ -39,8 +39,8 @@ SIGNATURES = {
     "mf_optim_chunk_elems": [],
     "mf_clip_grad_norm": [P, P, P, I, F, P, P, P],
     "mf_sgd_step": [P, P, P, L, I, P, P, P],
-    "mf_fedavg_pack": [P, L, P, L, P, P],
-    "mf_fedavg_unpack": [P, F, P, L, P, L, P],
+    "mf_fedavg_pack": [P, L, P, L, P, P, P],
+    "mf_fedavg_unpack": [P, P, L, P, L, P, P, P],
     "mf_nonfinite_flag": [P, L, I, P, P],
 }
 # functions that return a value, not a status

@@ -140,23 +140,42 @@ __global__ void sgd_kernel(T* __restrict__ p, T* __restrict__ g, T* __restrict__
 
 // bucket[0:n16] = float(p16), bucket[n16:n16+n32] = p32
 __global__ void pack_kernel(const f16* __restrict__ p16, int64_t n16, const float* __restrict__ p32, int64_t n32,
-                            float* __restrict__ bucket) {
+                            const int* __restrict__ invalid, float* __restrict__ bucket) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool bad = invalid && invalid[0] != 0;  // this client's weights are excluded (maple_fed.py:272-277)
   if (i < n16)
-    bucket[i] = (float)p16[i];
+    bucket[i] = bad ? 0.f : (float)p16[i];
   else if (i < n16 + n32)
-    bucket[i] = p32[i - n16];
+    bucket[i] = bad ? 0.f : p32[i - n16];
+  else if (i == n16 + n32)
+    bucket[i] = bad ? 0.f : 1.f;  // this client's vote in the valid-client count
 }
-
-// mean = sum / n ; value = fp16(mean) ; p16 = value, p32 = float(value)   (the `.half()` of
-// trainers/maple_fed.py:314 followed by load_state_dict into each parameter's dtype)
-__global__ void unpack_kernel(const float* __restrict__ bucket, float n_valid, f16* __restrict__ p16, int64_t n16,
-                              float* __restrict__ p32, int64_t n32) {
+// mean = sum / n_valid with n_valid = bucket[n16+n32] read on the device (no host sync); value =
+// fp16(mean); p16 = value, p32 = float(value)   (the `.half()` of trainers/maple_fed.py:314 followed
+// by load_state_dict into each parameter's dtype), and the value is kept as the new global copy
+// (g16/g32).  n_valid == 0 -> every client failed: the round is skipped and every client goes back
+// to the previous global weights (trainers/maple_fed.py:288-290 + the next round's broadcast).
+__global__ void unpack_kernel(const float* __restrict__ bucket, f16* __restrict__ p16, int64_t n16,
+                              float* __restrict__ p32, int64_t n32, f16* __restrict__ g16, float* __restrict__ g32) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const float n_valid = bucket[n16 + n32];
   if (i < n16) {
-    p16[i] = (f16)(bucket[i] / n_valid);
+    if (n_valid == 0.f) {
+      if (g16) p16[i] = g16[i];
+    } else {
+      const f16 v = (f16)(bucket[i] / n_valid);
+      p16[i] = v;
+      if (g16) g16[i] = v;
+    }
   } else if (i < n16 + n32) {
-    p32[i - n16] = r16(bucket[i] / n_valid);
+    const int64_t j = i - n16;
+    if (n_valid == 0.f) {
+      if (g32) p32[j] = g32[j];
+    } else {
+      const float v = r16(bucket[i] / n_valid);
+      p32[j] = v;
+      if (g32) g32[j] = v;
+    }
   }
 }
 
@@ -202,19 +221,19 @@ extern "C" int mf_sgd_step(void* p, void* g, void* buf, int64_t n, int is16, con
   return 0;
 }
 
-extern "C" int mf_fedavg_pack(const void* p16, int64_t n16, const float* p32, int64_t n32, float* bucket,
-                              void* stream) {
-  if (n16 + n32 <= 0) return 0;
-  pack_kernel<<<nblk(n16 + n32), 256, 0, (hipStream_t)stream>>>((const f16*)p16, n16, p32, n32, bucket);
+extern "C" int mf_fedavg_pack(const void* p16, int64_t n16, const float* p32, int64_t n32, const int* invalid_flag,
+                              float* bucket, void* stream) {
+  if (n16 < 0 || n32 < 0) return mf_set_error("mf_fedavg_pack: negative size", -1);
+  pack_kernel<<<nblk(n16 + n32 + 1), 256, 0, (hipStream_t)stream>>>((const f16*)p16, n16, p32, n32, invalid_flag,
+                                                                    bucket);
   MF_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int mf_fedavg_unpack(const float* bucket, float n_valid, void* p16, int64_t n16, float* p32, int64_t n32,
-                                void* stream) {
+extern "C" int mf_fedavg_unpack(const float* bucket, void* p16, int64_t n16, float* p32, int64_t n32, void* g16,
+                                float* g32, void* stream) {
   if (n16 + n32 <= 0) return 0;
-  if (!(n_valid >= 1.f)) return mf_set_error("mf_fedavg_unpack: n_valid must be >= 1", -1);
-  unpack_kernel<<<nblk(n16 + n32), 256, 0, (hipStream_t)stream>>>(bucket, n_valid, (f16*)p16, n16, p32, n32);
+  unpack_kernel<<<nblk(n16 + n32), 256, 0, (hipStream_t)stream>>>(bucket, (f16*)p16, n16, p32, n32, (f16*)g16, g32);
   MF_CHECK_LAUNCH();
   return 0;
 }

@@ -266,6 +266,7 @@ class MapleEngine:
                           True, 1)
         self._build_io()
         self.side = torch.cuda.Stream(device=self.device)
+        self.overlap_towers = True  # False: both towers on the current stream (isolated kernel timing)
         self.step_count = 0
         self.hyper = torch.tensor([0.0, cfg.momentum, cfg.weight_decay, 1.0], device=self.device, dtype=F32)
         self.momentum_initialised = False
@@ -480,11 +481,12 @@ class MapleEngine:
         smaller kernels fill the CUs the vision GEMMs leave idle."""
         self._prompt_learner_fwd()
         main = torch.cuda.current_stream(self.device)
-        self.side.wait_stream(main)
-        with torch.cuda.stream(self.side):
+        side = self.side if self.overlap_towers else main
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
             self._text_forward()
         self._vision_forward()
-        main.wait_stream(self.side)
+        main.wait_stream(side)
         ops.clip_head_fwd(self.img_feat, self.txt_feat, self.P["logit_scale"], self.img_n, self.txt_n, self.norms,
                           self.mm, self.logits)
         return self.logits
@@ -524,11 +526,12 @@ class MapleEngine:
                               self.label_in, self.P["logit_scale"], self.dmm, self.cos_ws, self.loss_out,
                               self.dimg_n, self.dtxt_n, self.dimg, self.dtxt)
         main = torch.cuda.current_stream(self.device)
-        self.side.wait_stream(main)
-        with torch.cuda.stream(self.side):
+        side = self.side if self.overlap_towers else main
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
             self._text_backward()
         self._vision_backward()
-        main.wait_stream(self.side)
+        main.wait_stream(side)
         self._prompt_learner_bwd()
 
     # ------------------------------------------------------------------ optimizer

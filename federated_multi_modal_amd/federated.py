@@ -27,10 +27,22 @@ import torch.distributed as dist
 from . import ops
 
 
+class _HipKernels:
+    """The device kernels FedAvgBucket drives (libmapfed.so)."""
+    nonfinite_flag = staticmethod(ops.nonfinite_flag)
+    fedavg_pack = staticmethod(ops.fedavg_pack)
+    fedavg_unpack = staticmethod(ops.fedavg_unpack)
+
+
 class FedAvgBucket:
-    def __init__(self, engine, group: Optional[dist.ProcessGroup] = None):
+    """`engine` needs: device, n16, n32, flat16 (fp16 trainables), flat32 (fp32 trainables) and
+    after_weights_loaded().  `kernels` defaults to the HIP kernels; tests substitute host
+    restatements to exercise the collective protocol on CPU ranks (gloo)."""
+
+    def __init__(self, engine, group: Optional[dist.ProcessGroup] = None, kernels=_HipKernels):
         self.e = engine
         self.group = group
+        self.k = kernels
         dev = engine.device
         n = engine.n16 + engine.n32
         # [bucket | count]: one contiguous buffer so the mean and the valid-client count travel in ONE
@@ -39,6 +51,9 @@ class FedAvgBucket:
         self.bucket = self.buf[:n]
         self.count = self.buf[n:]
         self.flag = torch.zeros(1, device=dev, dtype=torch.int32)
+        # the last global weights (what broadcast_weights would load): restored when a round fails
+        self.global16 = engine.flat16.detach().clone()
+        self.global32 = engine.flat32.detach().clone()
         self.work = None
 
     def _distributed(self) -> bool:
@@ -48,29 +63,29 @@ class FedAvgBucket:
         """Validity scan + pack + (async) all-reduce; returns immediately (overlap with test())."""
         e = self.e
         self.flag.zero_()
-        ops.nonfinite_flag(e.flat16, self.flag)
-        ops.nonfinite_flag(e.flat32, self.flag)
-        ops.fedavg_pack(e.flat16, e.flat32, self.bucket)
-        valid = (self.flag == 0).to(torch.float32)
-        self.bucket.mul_(valid)  # an invalid client contributes nothing (trainers/maple_fed.py:272-277)
-        self.count.copy_(valid)
+        self.k.nonfinite_flag(e.flat16, self.flag)
+        self.k.nonfinite_flag(e.flat32, self.flag)
+        # an invalid client contributes zeros and no vote (trainers/maple_fed.py:272-277)
+        self.k.fedavg_pack(e.flat16, e.flat32, self.flag, self.buf)
         self.work = None
         if self._distributed():
             self.work = dist.all_reduce(self.buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
-    def finish(self) -> int:
-        """Wait, then write the fp16-rounded mean into every trainable; returns n_valid (0 -> skipped)."""
+    def finish(self):
+        """Wait for the collective, then write the fp16-rounded mean into every trainable (device-side
+        n_valid; n_valid == 0 leaves the weights untouched).  No host synchronisation."""
         if self.work is not None:
             self.work.wait()
             self.work = None
-        n_valid = int(round(float(self.count.item())))
-        if n_valid == 0:
-            return 0  # every client failed: keep the global weights (trainers/maple_fed.py:288-290)
         e = self.e
-        ops.fedavg_unpack(self.bucket, float(n_valid), e.flat16, e.flat32)
+        self.k.fedavg_unpack(self.buf, e.flat16, e.flat32, self.global16, self.global32)
         e.after_weights_loaded()
-        return n_valid
+
+    def n_valid(self) -> int:
+        """Valid clients of the last round (host sync)."""
+        return int(round(float(self.count.item())))
 
     def run(self) -> int:
         self.start()
-        return self.finish()
+        self.finish()
+        return self.n_valid()

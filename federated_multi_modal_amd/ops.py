@@ -228,12 +228,14 @@ def sgd_step(p, g, buf, coef, hyper):
     call("mf_sgd_step", _p(p), _p(g), _p(buf), p.numel(), int(p.dtype == torch.float16), _p(coef), _p(hyper), _s())
 
 
-def fedavg_pack(p16, p32, bucket):
-    call("mf_fedavg_pack", _p(p16), p16.numel(), _p(p32), p32.numel(), _p(bucket), _s())
+def fedavg_pack(p16, p32, invalid_flag, bucket):
+    """bucket: n16 + n32 + 1 floats (last = this client's valid vote)."""
+    assert bucket.numel() == p16.numel() + p32.numel() + 1
+    call("mf_fedavg_pack", _p(p16), p16.numel(), _p(p32), p32.numel(), _p(invalid_flag), _p(bucket), _s())
 
 
-def fedavg_unpack(bucket, n_valid, p16, p32):
-    call("mf_fedavg_unpack", _p(bucket), float(n_valid), _p(p16), p16.numel(), _p(p32), p32.numel(), _s())
+def fedavg_unpack(bucket, p16, p32, g16=None, g32=None):
+    call("mf_fedavg_unpack", _p(bucket), _p(p16), p16.numel(), _p(p32), p32.numel(), _p(g16), _p(g32), _s())
 
 
 def nonfinite_flag(x, flag):

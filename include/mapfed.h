@@ -101,8 +101,14 @@ int mf_clip_grad_norm(const void* g16, const float* g32, const void* chunks, int
 /* coef: the clip output (coef at [1]); hyper (device): {lr, momentum, weight_decay, first_step}   */
 int mf_sgd_step(void* p, void* g, void* buf, int64_t n, int is16, const float* coef, const float* hyper,
                 void* stream);
-int mf_fedavg_pack(const void* p16, int64_t n16, const float* p32, int64_t n32, float* bucket, void* stream);
-int mf_fedavg_unpack(const float* bucket, float n_valid, void* p16, int64_t n16, float* p32, int64_t n32,
+/* bucket[0:n16+n32] = this client's trainables as fp32 (0 if *invalid_flag), bucket[n16+n32] = its vote
+ * (1 valid / 0 invalid); after an all-reduce(SUM) of the n16+n32+1 floats, unpack writes
+ * fp16(sum / n_valid) into every trainable and into the global copy g16/g32, n_valid read from
+ * bucket[n16+n32] on the device; n_valid == 0 (every client failed) restores the trainables from g16/g32.
+ * Replaces: safe_average_weights + broadcast_weights' load_state_dict (trainers/maple_fed.py:309-315,327-331). */
+int mf_fedavg_pack(const void* p16, int64_t n16, const float* p32, int64_t n32, const int* invalid_flag,
+                   float* bucket, void* stream);
+int mf_fedavg_unpack(const float* bucket, void* p16, int64_t n16, float* p32, int64_t n32, void* g16, float* g32,
                      void* stream);
 int mf_nonfinite_flag(const void* x, int64_t n, int is16, int* flag, void* stream);
 

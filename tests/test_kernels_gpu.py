@@ -325,3 +325,33 @@ def test_sgd_and_clip(dev):
     ops.sgd_step(p32, g32, b32, out, hyper)
     assert (p16 != rp16.detach()).float().mean().item() < 1e-3
     torch.testing.assert_close(p32, rp32.detach(), rtol=1e-6, atol=1e-7)
+
+
+def test_fedavg_kernels_single_client(dev):
+    """World size 1 through the HIP kernels: the mean of one client is its own weights rounded to
+    fp16 (the `.half()` of trainers/maple_fed.py:314 on fp32 keys); a NaN client restores the
+    previous global weights (round skipped)."""
+    from federated_multi_modal_amd.federated import FedAvgBucket
+
+    class Eng:
+        device = dev
+        n16, n32 = 1000, 777
+        reloaded = 0
+
+        def after_weights_loaded(self):
+            self.reloaded += 1
+
+    e = Eng()
+    e.flat16 = torch.randn(e.n16, device=dev).half()
+    e.flat32 = torch.randn(e.n32, device=dev) * 3
+    fed = FedAvgBucket(e)
+    g16, g32 = e.flat16.clone(), e.flat32.clone()
+    e.flat32.add_(1e-3)  # local training moved the weights
+    local32 = e.flat32.clone()
+    assert fed.run() == 1
+    assert torch.equal(e.flat16, g16)
+    assert torch.equal(e.flat32, local32.half().float())
+    new32 = e.flat32.clone()
+    e.flat32[5] = float("nan")
+    assert fed.run() == 0
+    assert torch.equal(e.flat32, new32) and torch.equal(e.flat16, g16)
