@@ -198,7 +198,66 @@ __global__ void normalize_bwd_kernel(const f16* __restrict__ x, const f16* __res
   }
 }
 
+// eval argmax (trainers/maple.py:674-677): pred[b] = argmax_k logits[b,k] (first maximum, NaN counts as
+// the maximum like torch.argmax); acc[0] += #(pred == label), acc[1] += B.  One wave per row.
+__global__ void argmax_correct_kernel(const f16* __restrict__ logits, int B, int K, const int64_t* __restrict__ label,
+                                      int64_t* __restrict__ pred, float* __restrict__ acc) {
+  __shared__ int s_ok[16];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int ok = 0;
+  for (int b = w; b < B; b += 16) {
+    float best = -INFINITY;
+    int bi = -1;  // no candidate yet
+    for (int k = lane; k < K; k += 64) {  // ascending k: on ties the first index stays
+      const float v = (float)logits[(int64_t)b * K + k];
+      const bool better = bi < 0 || (isnan(v) ? !isnan(best) : (!isnan(best) && v > best));
+      if (better) {
+        best = v;
+        bi = k;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      bool take;
+      if (oi < 0)
+        take = false;
+      else if (bi < 0)
+        take = true;
+      else if (isnan(ob) || isnan(best))
+        take = isnan(ob) && (!isnan(best) || oi < bi);
+      else
+        take = ob > best || (ob == best && oi < bi);
+      if (take) {
+        best = ob;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      if (pred) pred[b] = bi;
+      if (label) ok += (bi == (int)label[b]);
+    }
+  }
+  if (lane == 0) s_ok[w] = ok;
+  __syncthreads();
+  if (threadIdx.x == 0 && acc) {
+    int tot = 0;
+    for (int i = 0; i < 16; ++i) tot += s_ok[i];
+    acc[0] += (float)tot;
+    acc[1] += (float)B;
+  }
+}
+
 }  // namespace
+
+extern "C" int mf_argmax_correct(const void* logits, int B, int K, const int64_t* label, int64_t* pred, float* acc,
+                                 void* stream) {
+  if (B <= 0) return 0;
+  argmax_correct_kernel<<<1, 1024, 0, (hipStream_t)stream>>>((const f16*)logits, B, K, label, pred, acc);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
 
 // workspace floats needed: 2*B (cos norms) + (B+K) (feature norms)
 extern "C" int mf_clip_head_fwd(const void* img, const void* txt, int B, int K, int D, const float* logit_scale,

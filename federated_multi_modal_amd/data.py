@@ -1,0 +1,100 @@
+"""Per-client data feeding for the federated MaPLe path (the role of trainers/client_datamanager.py
+and the class-union logic of trainers/maple_fed.py:48-159).
+
+The reference reads PatternNet / UcMerced / EuroSAT images from disk through Dassl loaders with
+PIL transforms (random_resized_crop, flip, CLIP normalisation).  Real datasets are out of scope
+here; each client instead owns a seeded synthetic split of the same shape
+-- normalised 224x224x3 images and labels over the unified class list -- generated once by the
+portable PRNG (federated_multi_modal_amd.synthetic) and kept resident in HBM, so a training step
+reads its batch from device memory (no host->device copy on the hot path).
+
+Loaders yield the reference's batch dicts: {"img": [B,3,224,224] fp32, "label": [B] int64,
+"caption": list[str]} (trainers/maple.py:537-545).  The train loader reshuffles every epoch with the
+client's own generator (RandomSampler semantics, drop_last as Dassl's train loader:
+len(train_x) >= batch).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Iterator, List, Sequence
+
+import zlib
+
+import numpy as np
+import torch
+
+from . import synthetic as syn
+
+# Dataset shapes of the reference's clients (number of classes) and the shapes BASELINE.json names
+DATASET_CLASSES = {"PatternNet": 38, "Ucmerced": 21, "EuroSAT": 10, "ImageNet": 1000}
+
+
+def unified_classnames(datasets: Sequence[str], seed: int = 0) -> List[str]:
+    """Sorted union of the clients' class names (trainers/maple_fed.py:98-107).  Synthetic names stand
+    in for the dataset folders; the union of distinct synthetic lists is their concatenation."""
+    names = []
+    for i, ds in enumerate(datasets):
+        names += [f"{ds.lower()}_{c}" for c in syn.synthetic_classnames(DATASET_CLASSES[ds], seed + 17 * i)]
+    return sorted(set(names))
+
+
+@dataclass
+class _Split:
+    images: torch.Tensor  # [N,3,R,R] fp32, device
+    labels: torch.Tensor  # [N] int64, device
+
+
+class _Loader:
+    def __init__(self, split: _Split, batch: int, shuffle: bool, drop_last: bool, gen: torch.Generator):
+        self.s, self.batch, self.shuffle, self.drop_last, self.gen = split, batch, shuffle, drop_last, gen
+
+    def __len__(self):
+        n = self.s.labels.numel()
+        return n // self.batch if self.drop_last else (n + self.batch - 1) // self.batch
+
+    def __iter__(self) -> Iterator[Dict[str, object]]:
+        n = self.s.labels.numel()
+        order = torch.randperm(n, generator=self.gen) if self.shuffle else torch.arange(n)
+        order = order.to(self.s.labels.device)
+        for i in range(len(self)):
+            idx = order[i * self.batch:(i + 1) * self.batch]
+            yield {"img": self.s.images.index_select(0, idx), "label": self.s.labels.index_select(0, idx),
+                   "caption": [""] * idx.numel(), "index": idx}
+
+
+class SyntheticClientDataManager:
+    """ClientDataManager stand-in: .train_loader / .test_loader / .num_classes / .lab2cname."""
+
+    def __init__(self, client_id: int, classnames: List[str], n_train: int, n_test: int, train_batch: int,
+                 test_batch: int, device, seed: int = 0, image_resolution: int = 224):
+        self.client_id = client_id
+        self._classnames = list(classnames)
+        K = len(classnames)
+        self.device = torch.device(device)
+
+        def make(tag: str, n: int) -> _Split:
+            imgs, labs = [], []
+            for s0 in range(0, n, 64):  # generate in chunks (host memory)
+                b = syn.client_batch(seed, client_id, zlib.crc32(tag.encode()) + s0, min(64, n - s0), K,
+                                     image_resolution)
+                imgs.append(torch.from_numpy(b.images).to(self.device))
+                labs.append(torch.from_numpy(b.labels).to(self.device))
+            return _Split(torch.cat(imgs), torch.cat(labs))
+
+        self.train = make("train", n_train)
+        self.test = make("test", n_test)
+        g = torch.Generator().manual_seed(seed * 1000 + client_id)
+        self.train_loader = _Loader(self.train, train_batch, shuffle=True, drop_last=n_train >= train_batch, gen=g)
+        self.test_loader = _Loader(self.test, test_batch, shuffle=False, drop_last=False, gen=g)
+
+    @property
+    def num_classes(self) -> int:
+        return len(self._classnames)
+
+    @property
+    def lab2cname(self) -> Dict[int, str]:
+        return {i: c for i, c in enumerate(self._classnames)}
+
+    @property
+    def classnames(self) -> List[str]:
+        return self._classnames

@@ -112,19 +112,35 @@ def synthetic_state(cfg: EngineConfig) -> Dict[str, np.ndarray]:
     """Synthetic values for every spec, keyed by CustomCLIP parameter name (numpy fp32)."""
     d = cfg.dims
     sd = syn.clip_state_dict(cfg.seed, d, vision_layers=d.vision_layers, text_layers=d.text_layers)
+    return engine_state_from_clip(sd, cfg)
+
+
+def engine_state_from_clip(clip_sd: Dict[str, np.ndarray], cfg: EngineConfig,
+                           prompt_learner: Optional[Dict[str, np.ndarray]] = None) -> Dict[str, np.ndarray]:
+    """Map a CLIP checkpoint state dict (keys of clip/model.py CLIP: visual.*, transformer.*,
+    positional_embedding, ln_final.*, text_projection, token_embedding.weight, logit_scale) onto the
+    engine's CustomCLIP parameter names (trainers/maple.py:44-58,221-229), the way build_model +
+    CustomCLIP wire it (clip/model.py:750-793).  ctx is initialised from the token embedding of
+    CTX_INIT (trainers/maple.py:96-103); the other prompt-learner tensors come from
+    `prompt_learner` (names without the prefix) or the synthetic generator.  logit_scale is MaPLe's
+    own ln(1/0.07) (trainers/maple.py:227), not the checkpoint's."""
     out: Dict[str, np.ndarray] = {}
-    for k, v in sd.items():
-        if k == "logit_scale":
-            continue
+    for k, v in clip_sd.items():
+        v = np.asarray(v, dtype=np.float32)
         if k.startswith("visual."):
             out["image_encoder." + k[7:]] = v
         elif k in ("positional_embedding", "ln_final.weight", "ln_final.bias", "text_projection") or \
                 k.startswith("transformer."):
             out["text_encoder." + k] = v
-    init = syn.tokenize(cfg.ctx_init)
-    out["prompt_learner.ctx"] = syn.token_embedding_rows(cfg.seed, init[0, 1:1 + cfg.n_ctx])
-    for k, v in syn.prompt_learner_params(cfg.seed, cfg.prompt_depth, cfg.n_ctx).items():
-        out["prompt_learner." + k] = v
+    init = syn.tokenize(cfg.ctx_init)[0, 1:1 + cfg.n_ctx]
+    if "token_embedding.weight" in clip_sd:
+        out["prompt_learner.ctx"] = np.asarray(clip_sd["token_embedding.weight"], dtype=np.float32)[init]
+    else:
+        out["prompt_learner.ctx"] = syn.token_embedding_rows(cfg.seed, init)
+    pl = prompt_learner if prompt_learner is not None else syn.prompt_learner_params(cfg.seed, cfg.prompt_depth,
+                                                                                     cfg.n_ctx)
+    for k, v in pl.items():
+        out["prompt_learner." + k] = np.asarray(v, dtype=np.float32)
     out["logit_scale"] = np.array(math.log(1 / 0.07), dtype=np.float32)
     return out
 
@@ -247,16 +263,29 @@ class _Tower:
 class MapleEngine:
     """One federated client on one GPU."""
 
-    def __init__(self, cfg: EngineConfig, device="cuda", state: Optional[Dict[str, np.ndarray]] = None):
+    def __init__(self, cfg: EngineConfig, device="cuda", state: Optional[Dict[str, np.ndarray]] = None,
+                 shared: Optional["MapleEngine"] = None):
+        """state: parameter values by CustomCLIP name (default: the synthetic generator).
+        shared: another engine whose parameters (and gradients, optimizer state, text constants)
+        this one uses -- e.g. the test-batch engine next to a training engine (different batch
+        size, same model), as trainers/maple.py:660-681 evaluates the model being trained."""
         self.cfg = cfg
         self.device = torch.device(device)
         d = cfg.dims
         self.B, self.K, self.J = cfg.batch, len(cfg.classnames), cfg.prompt_depth
         assert 1 <= self.J <= 12, "PROMPT_DEPTH must be in [1, 12]"
         self.specs = reference_param_specs(cfg)
-        vals = state if state is not None else synthetic_state(cfg)
-        self._build_params(vals)
-        self._build_text_constants()
+        if shared is None:
+            vals = state if state is not None else synthetic_state(cfg)
+            self._build_params(vals)
+            self._build_text_constants()
+            self.hyper = torch.tensor([0.0, cfg.momentum, cfg.weight_decay, 1.0], device=self.device, dtype=F32)
+        else:
+            assert shared.K == self.K and shared.J == self.J and shared.device == self.device
+            for a in ("n16", "n32", "flat16", "flat32", "gflat16", "gflat32", "mom16", "mom32", "P", "G",
+                      "trainable_names", "conv_w", "chunks", "nchunks", "norm_part", "clip_out", "WT", "projT",
+                      "text_projT", "tokenized", "token_prefix", "token_suffix", "eot_rows", "hyper"):
+                setattr(self, a, getattr(shared, a))
         G2 = d.grid * d.grid
         self.Lv = G2 + 1 + cfg.n_ctx
         self.G2 = G2
@@ -268,7 +297,6 @@ class MapleEngine:
         self.side = torch.cuda.Stream(device=self.device)
         self.overlap_towers = True  # False: both towers on the current stream (isolated kernel timing)
         self.step_count = 0
-        self.hyper = torch.tensor([0.0, cfg.momentum, cfg.weight_decay, 1.0], device=self.device, dtype=F32)
         self.momentum_initialised = False
 
     # ------------------------------------------------------------------ parameters
@@ -342,9 +370,13 @@ class MapleEngine:
         for n, t in self.WT.items():
             if all_layers or ".resblocks.11." in n:
                 ops.transpose(self.P[n], t)
-        if all_layers:  # frozen head projections (x @ proj == NT GEMM with proj^T)
-            self.projT = self.P["image_encoder.proj"].t().contiguous()
-            self.text_projT = self.P["text_encoder.text_projection"].t().contiguous()
+        if all_layers:  # frozen head projections (x @ proj == NT GEMM with proj^T); in place, so that
+            # pointers captured in a hipGraph stay valid
+            if not hasattr(self, "projT"):
+                self.projT = torch.empty_like(self.P["image_encoder.proj"].t().contiguous())
+                self.text_projT = torch.empty_like(self.P["text_encoder.text_projection"].t().contiguous())
+            ops.transpose(self.P["image_encoder.proj"], self.projT)
+            ops.transpose(self.P["text_encoder.text_projection"], self.text_projT)
 
     def _build_text_constants(self):
         """token prefix / suffix buffers and the EOT gather index (trainers/maple.py:136-149)."""
@@ -474,6 +506,13 @@ class MapleEngine:
                           self.post_mean, self.post_rstd, row_index=self.cls_rows)
         ops.gemm_nt(self.vis_post, self.projT, self.img_feat, epilogue=ops.EPI_NONE)
 
+    def eval_batch(self, labels: Optional[torch.Tensor], acc: torch.Tensor, pred: Optional[torch.Tensor] = None):
+        """One test batch (trainers/maple.py:671-677): logits, argmax, correct count accumulated in
+        acc (device float[2]: correct, total).  Images must already be in img_in."""
+        logits = self.forward()
+        ops.argmax_correct(logits, labels, pred, acc)
+        return logits
+
     def forward(self):
         """CustomCLIP.forward up to the logits (eval path, trainers/maple.py:304-346).  The text and
         vision towers are independent until the head: the text tower runs on a side stream, forked
@@ -580,7 +619,41 @@ class MapleEngine:
         return float(v[0])
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
+        """CustomCLIP parameter names -> device tensors (the reference's model.state_dict() minus the
+        clip_model2.* aliases and buffers, see reference_state_dict)."""
         return {n: t for n, t in self.P.items()}
+
+    def reference_state_dict(self) -> Dict[str, torch.Tensor]:
+        """The reference's full CustomCLIP state-dict key set (trainers/maple.py:221-229): parameters,
+        the prompt learner's token_prefix/suffix buffers and the clip_model2.* aliases of the CLIP
+        weights the towers share (634 keys at J=9, token_embedding excluded)."""
+        out = dict(self.state_dict())
+        out["prompt_learner.token_prefix"] = self.token_prefix
+        out["prompt_learner.token_suffix"] = self.token_suffix
+        for n, t in self.P.items():
+            if n.startswith("image_encoder."):
+                out["clip_model2.visual." + n[len("image_encoder."):]] = t
+            elif n.startswith("text_encoder."):
+                out["clip_model2." + n[len("text_encoder."):]] = t
+        out["clip_model2.logit_scale"] = self.P["logit_scale"]
+        return out
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        """load_state_dict of the reference model (trainers/maple_fed.py:329): every parameter name
+        must be present when strict; values are cast to each parameter's dtype."""
+        missing = [n for n in self.P if n not in sd]
+        if strict and missing:
+            raise RuntimeError(f"Missing key(s) in state_dict: {missing[:5]}...")
+        frozen_changed = False
+        with torch.no_grad():
+            for n, t in self.P.items():
+                if n in sd:
+                    t.copy_(torch.as_tensor(sd[n]).reshape(t.shape).to(device=t.device, dtype=t.dtype))
+                    frozen_changed |= n not in self.trainable_names
+            if "prompt_learner.token_prefix" in sd:
+                self.token_prefix.copy_(sd["prompt_learner.token_prefix"])
+                self.token_suffix.copy_(sd["prompt_learner.token_suffix"])
+        self.refresh_transposes(all_layers=frozen_changed)
 
     def trainable_state(self) -> Dict[str, torch.Tensor]:
         return {n: self.P[n] for n in self.trainable_names}

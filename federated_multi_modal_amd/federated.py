@@ -59,8 +59,10 @@ class FedAvgBucket:
     def _distributed(self) -> bool:
         return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
 
-    def start(self):
-        """Validity scan + pack + (async) all-reduce; returns immediately (overlap with test())."""
+    def start(self, collective: bool = True):
+        """Validity scan + pack + (async) all-reduce; returns immediately (overlap with test()).
+        collective=False packs only (several clients in one process reduce their buckets with
+        reduce_local)."""
         e = self.e
         self.flag.zero_()
         self.k.nonfinite_flag(e.flat16, self.flag)
@@ -68,7 +70,7 @@ class FedAvgBucket:
         # an invalid client contributes zeros and no vote (trainers/maple_fed.py:272-277)
         self.k.fedavg_pack(e.flat16, e.flat32, self.flag, self.buf)
         self.work = None
-        if self._distributed():
+        if collective and self._distributed():
             self.work = dist.all_reduce(self.buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def finish(self):
@@ -89,3 +91,16 @@ class FedAvgBucket:
         self.start()
         self.finish()
         return self.n_valid()
+
+
+def reduce_local(buckets) -> None:
+    """In-process stand-in for the all-reduce when several clients share one process/GPU (the
+    reference's sequential clients, trainers/maple_fed.py:247): SUM of every packed bucket, written
+    back into each of them.  Clients are added in client order, like torch.stack(...).mean(0)."""
+    if len(buckets) < 2:
+        return
+    total = buckets[0].buf.clone()
+    for b in buckets[1:]:
+        total.add_(b.buf)
+    for b in buckets:
+        b.buf.copy_(total)

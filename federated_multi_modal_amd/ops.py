@@ -215,6 +215,11 @@ def clip_loss_fwd_bwd(img, txt, img_n, txt_n, norms, logits, label, logit_scale,
          _p(logit_scale), _p(dmm), _p(cos_ws), _p(loss_out), _p(dimg_n), _p(dtxt_n), _p(dimg), _p(dtxt), _s())
 
 
+def argmax_correct(logits, label=None, pred=None, acc=None):
+    B, K = logits.shape
+    call("mf_argmax_correct", _p(logits), B, K, _p(label), _p(pred), _p(acc), _s())
+
+
 def optim_chunk_elems() -> int:
     return call("mf_optim_chunk_elems")
 

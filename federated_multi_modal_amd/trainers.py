@@ -1,0 +1,533 @@
+"""The reference's trainer plugin API for the federated MaPLe path, on the MI355X engine.
+
+Mirrors (same class names, registry, method names, return dicts and error behaviour):
+  * Dassl's TRAINER_REGISTRY / build_trainer / TrainerX subset used by train.py:177-185
+  * MaPLe(TrainerX)            trainers/maple.py:384-716   (one federated client)
+  * MaPLeFederated(TrainerX)   trainers/maple_fed.py:24-500 (round loop, FedAvg, checkpoints)
+
+What runs where:
+  * every forward/backward/optimizer step is MapleEngine (libmapfed.so kernels), replayed as one
+    hipGraph per step; the loss, NaN flags and accuracy counters stay on the device and are read
+    once per epoch instead of ~150 host syncs per step (trainers/maple.py:601-615);
+  * the LR schedule is Dassl's, evaluated on the host (schedule.py) and handed to the SGD kernel;
+  * FedAvg is FedAvgBucket: one client per rank with an RCCL all-reduce when launched with
+    torch.distributed (WORLD_SIZE == FED.NUM_CLIENTS), or the reference's sequential clients in one
+    process (their buckets summed in client order).
+
+Error behaviour kept: NaN/Inf loss -> RuntimeError("NaN/Inf in total loss") from run_epoch
+(caught per client by the round loop, trainers/maple_fed.py:262-265); non-finite inputs ->
+ValueError (trainers/maple.py:526-535, not caught); kernel failures -> RuntimeError (MapfedError).
+"""
+from __future__ import annotations
+
+import os
+import os.path as osp
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+from .data import DATASET_CLASSES, SyntheticClientDataManager, unified_classnames
+from .engine import EngineConfig, MapleEngine
+from .federated import FedAvgBucket, reduce_local
+from .schedule import HostLR
+
+
+class Registry:
+    """Dassl's Registry: name -> class, `@TRAINER_REGISTRY.register()`."""
+
+    def __init__(self, name: str):
+        self.name, self._map = name, {}
+
+    def register(self, obj=None):
+        def deco(o):
+            if o.__name__ in self._map:
+                raise KeyError(f'An object named "{o.__name__}" was already registered in "{self.name}" registry')
+            self._map[o.__name__] = o
+            return o
+        return deco(obj) if obj is not None else deco
+
+    def get(self, name: str):
+        if name not in self._map:
+            raise KeyError(f'Object name "{name}" does not exist in "{self.name}" registry')
+        return self._map[name]
+
+    def registered_names(self):
+        return list(self._map)
+
+
+TRAINER_REGISTRY = Registry("TRAINER")
+
+
+def build_trainer(cfg):
+    """dassl.engine.build_trainer (train.py:177)."""
+    return TRAINER_REGISTRY.get(cfg.TRAINER.NAME)(cfg)
+
+
+def _device(cfg) -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("the MI355X trainers need a GPU (libmapfed.so kernels); none is visible")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return torch.device("cuda", local)
+
+
+class TrainerX:
+    """The part of Dassl's SimpleTrainer/TrainerX the MaPLe trainers rely on."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self._models: Dict[str, object] = {}
+        self._optims: Dict[str, object] = {}
+        self._scheds: Dict[str, object] = {}
+        self.start_epoch = self.epoch = 0
+        self.max_epoch = cfg.OPTIM.MAX_EPOCH
+        self.output_dir = cfg.OUTPUT_DIR
+        if not hasattr(self, "device"):
+            self.device = _device(cfg)
+        self.build_data_loader()
+        self.build_model()
+
+    def build_data_loader(self):
+        pass
+
+    def build_model(self):
+        raise NotImplementedError
+
+    def register_model(self, name="model", model=None, optim=None, sched=None):
+        self._models[name] = model
+        self._optims[name] = optim
+        self._scheds[name] = sched
+
+    def get_model_names(self, names=None):
+        names_real = list(self._models.keys())
+        if names is not None:
+            names = [names] if isinstance(names, str) else names
+            for n in names:
+                assert n in names_real
+            return names
+        return names_real
+
+
+class _ModelView:
+    """The `model` attribute of a client (CustomCLIP stand-in): state_dict / load_state_dict /
+    train / eval / parameters counts, backed by the engine's device tensors."""
+
+    def __init__(self, engine: MapleEngine):
+        self.e = engine
+        self.training = True
+
+    def state_dict(self):
+        return self.e.reference_state_dict()
+
+    def load_state_dict(self, sd, strict: bool = True):
+        self.e.load_state_dict(sd, strict=strict)
+
+    def train(self, mode: bool = True):
+        self.training = mode
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def trainable_parameters(self):
+        return self.e.trainable_state()
+
+
+@TRAINER_REGISTRY.register()
+class MaPLe(TrainerX):
+    """One federated client (trainers/maple.py:384-716) on one GPU."""
+
+    def __init__(self, cfg, client_id=None, classnames=None, dm=None, device=None):
+        self.client_id = client_id
+        self.nan_count = 0
+        self.total_batches = 0
+        self.classnames = classnames
+        self.dm = dm
+        if device is not None:
+            self.device = torch.device(device)
+        self.lr_history: List[float] = []
+        self.grad_norms: List[float] = []
+        self._built = False
+        self.check_cfg(cfg)
+        super().__init__(cfg)
+
+    def check_cfg(self, cfg):
+        assert cfg.TRAINER.MAPLE.PREC in ["fp16", "fp32", "amp"], f"Invalid precision setting: {cfg.TRAINER.MAPLE.PREC}"
+        if cfg.TRAINER.MAPLE.PREC != "fp16":
+            # the reference crashes for fp32/amp on its own path (hard-coded .half())
+            raise NotImplementedError("the MaPLe hot path runs the reference's fp16 precision (PREC=fp16)")
+
+    def build_data_loader(self):
+        if self.dm is None:  # standalone client: one synthetic split over the configured classes
+            K = self.cfg.MODEL.NUM_CLASSES or len(self.classnames or []) or DATASET_CLASSES["EuroSAT"]
+            if self.classnames is None:
+                self.classnames = unified_classnames(["EuroSAT"])[:K]
+            self.dm = SyntheticClientDataManager(self.client_id or 0, self.classnames, n_train=16 * len(
+                self.classnames), n_test=len(self.classnames) * 4, train_batch=self.cfg.DATALOADER.TRAIN_X.BATCH_SIZE,
+                test_batch=self.cfg.DATALOADER.TEST.BATCH_SIZE, device=self.device, seed=max(self.cfg.SEED, 0))
+
+    def build_model(self):
+        """trainers/maple.py:421-524: CLIP ViT-B/16 + CustomCLIP, freeze policy (:447-479), SGD + LR
+        schedule (:498-499).  Weights: MODEL.INIT_WEIGHTS (a CLIP checkpoint / state dict file) when
+        given, else the seeded synthetic CLIP (the download of clip/clip.py:29-68 is offline)."""
+        if self._built:
+            return
+        cfg = self.cfg
+        mcfg = cfg.TRAINER.MAPLE
+        classnames = self.classnames
+        state = None
+        if cfg.MODEL.INIT_WEIGHTS:
+            state = _load_clip_weights(cfg.MODEL.INIT_WEIGHTS, cfg, classnames, mcfg)
+        ecfg = EngineConfig(batch=cfg.DATALOADER.TRAIN_X.BATCH_SIZE, classnames=list(classnames),
+                            prompt_depth=mcfg.PROMPT_DEPTH, seed=max(cfg.SEED, 0), n_ctx=mcfg.N_CTX,
+                            ctx_init=mcfg.CTX_INIT, momentum=cfg.OPTIM.MOMENTUM,
+                            weight_decay=cfg.OPTIM.WEIGHT_DECAY)
+        if cfg.OPTIM.NAME != "sgd":
+            raise NotImplementedError(f"optimizer {cfg.OPTIM.NAME}: the MaPLe configs use sgd")
+        self.engine = MapleEngine(ecfg, device=self.device, state=state)
+        self._eval_engine: Optional[MapleEngine] = None
+        self.model = _ModelView(self.engine)
+        self.optim = HostLR(cfg.OPTIM)          # param_groups[0]['lr'] and the scheduler
+        self.sched = self.optim.sched
+        self.scaler = None
+        self.register_model(f"MultiModalPromptLearner_{self.client_id}", self.model, self.optim, self.sched)
+        self._graph = None
+        self._loss_sum = torch.zeros(1, device=self.device)
+        self._bad = torch.zeros(1, device=self.device)
+        self._acc = torch.zeros(2, device=self.device)
+        self.lr_history = [self.optim.lr]
+        self._built = True
+
+    # ---------------------------------------------------------------- training
+    def check_tensor_validity(self, tensor, name):
+        """trainers/maple.py:526-535."""
+        if tensor is None:
+            raise ValueError(f"Null tensor: {name}")
+        if not isinstance(tensor, torch.Tensor):
+            raise TypeError(f"Invalid tensor type: {name}")
+        if tensor.is_floating_point() and not torch.isfinite(tensor).all():
+            raise ValueError(f"NaN/Inf values in {name}")
+
+    def parse_batch_train(self, batch):
+        return batch["img"], batch["label"], batch.get("caption")
+
+    def _load(self, image, label):
+        e = self.engine
+        if image.shape[0] != e.B:
+            raise ValueError(f"batch of {image.shape[0]} images; the client engine is built for {e.B}")
+        if label.is_floating_point():
+            raise NotImplementedError("soft (float) labels: the KL-divergence branch of trainers/maple.py:356-360")
+        e.img_in.copy_(image, non_blocking=True)
+        e.label_in.copy_(label, non_blocking=True)
+
+    def _step_async(self, batch):
+        """One forward_backward without host synchronisation; the loss accumulates on the device."""
+        image, label, _ = self.parse_batch_train(batch)
+        self.total_batches += 1
+        self._load(image, label)
+        e = self.engine
+        e.set_lr(self.optim.lr)
+        if self._graph is None:
+            e.train_step()          # first step eager: creates the momentum buffers
+            self._graph = e.capture_train_step()
+        else:
+            self._graph.replay()
+        self._loss_sum.add_(e.loss_out[0:1])
+        self._bad.add_(e.loss_out[3:4])
+
+    def forward_backward(self, batch):
+        """trainers/maple.py:547-627: returns {"loss": float} (one host sync, like loss.item())."""
+        image, label, _ = self.parse_batch_train(batch)
+        self.check_tensor_validity(image, "input image")
+        self.check_tensor_validity(label, "input label")
+        before = float(self._loss_sum.item())
+        self._step_async(batch)
+        loss = float(self._loss_sum.item()) - before
+        if self.engine.loss_out[3].item() != 0.0:
+            raise RuntimeError("NaN/Inf in total loss")
+        return {"loss": loss}
+
+    def run_epoch(self, epoch):
+        """trainers/maple.py:629-653: one pass over the train loader, update_lr, test()."""
+        self.model.train()
+        self._loss_sum.zero_()
+        self._bad.zero_()
+        steps = 0
+        for batch_idx, batch in enumerate(self.dm.train_loader):
+            self.batch_idx = batch_idx
+            self._step_async(batch)
+            steps += 1
+        if self._bad.item() != 0.0:  # NaN/Inf loss in this epoch (trainers/maple.py:375-376)
+            raise RuntimeError("NaN/Inf in total loss")
+        self.update_lr()
+        local = self.test()
+        avg_loss = float(self._loss_sum.item()) / max(1, steps)
+        print(f"[Client {self.client_id}] Epoch {epoch} done. Loss={avg_loss:.4f}, Acc={local['accuracy']:.2f}%")
+        return {"avg_loss": avg_loss}
+
+    def update_lr(self):
+        if self.sched is not None:
+            self.optim.step()
+            self.sched = self.optim.sched
+            lr = self.optim.lr
+            if lr != self.lr_history[-1]:
+                self.lr_history.append(lr)
+
+    # ---------------------------------------------------------------- evaluation
+    def _evaluator(self, batch_size: int) -> MapleEngine:
+        if self._eval_engine is None or self._eval_engine.B != batch_size:
+            ecfg = EngineConfig(batch=batch_size, classnames=self.engine.cfg.classnames,
+                                prompt_depth=self.engine.J, seed=self.engine.cfg.seed, n_ctx=self.engine.cfg.n_ctx,
+                                ctx_init=self.engine.cfg.ctx_init)
+            self._eval_engine = MapleEngine(ecfg, device=self.device, shared=self.engine)
+        return self._eval_engine
+
+    def test(self, evaluate_train: bool = False):
+        """trainers/maple.py:660-681: accuracy (%) over the test loader; one host sync at the end."""
+        self.model.eval()
+        loader = self.dm.test_loader
+        ev = self._evaluator(loader.batch)
+        self._acc.zero_()
+        for batch in loader:
+            x, y, _ = self.parse_batch_train(batch)
+            n = y.numel()
+            if n == ev.B:
+                ev.img_in.copy_(x)
+                ev.eval_batch(y, self._acc)
+            else:  # ragged last batch: pad the static buffer, count only the real rows
+                ev.img_in.zero_()
+                ev.img_in[:n].copy_(x)
+                logits = ev.forward()
+                ops.argmax_correct(logits[:n], y, None, self._acc)
+        correct, total = self._acc.tolist()
+        acc = 100.0 * correct / total if total > 0 else 0.0
+        print(f"[Client {self.client_id}] Test Accuracy: {acc:.2f}%")
+        self.model.train()
+        return {"accuracy": acc}
+
+    def load_model(self, directory, epoch=None):
+        """trainers/maple.py:685-716."""
+        if not directory:
+            print("Note that load_model() is skipped as no pretrained model is given")
+            return
+        model_file = "model-best.pth.tar" if epoch is None else f"model.pth.tar-{epoch}"
+        for name in self.get_model_names():
+            path = osp.join(directory, name, model_file)
+            if not osp.exists(path):
+                raise FileNotFoundError(f"Model not found at '{path}'")
+            ckpt = torch.load(path, map_location="cpu", weights_only=True)
+            sd = ckpt["state_dict"]
+            sd.pop("prompt_learner.token_prefix", None)
+            sd.pop("prompt_learner.token_suffix", None)
+            self._models[name].load_state_dict(sd, strict=False)
+
+
+def _load_clip_weights(path, cfg, classnames, mcfg):
+    """A CLIP state dict saved with torch.save (loaded with weights_only=True: no code runs)."""
+    import numpy as np
+    from .engine import engine_state_from_clip
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    if isinstance(sd, dict) and "state_dict" in sd:
+        sd = sd["state_dict"]
+    ecfg = EngineConfig(batch=1, classnames=list(classnames), prompt_depth=mcfg.PROMPT_DEPTH, seed=max(cfg.SEED, 0),
+                        n_ctx=mcfg.N_CTX, ctx_init=mcfg.CTX_INIT)
+    return engine_state_from_clip({k: v.float().numpy() for k, v in sd.items()}, ecfg)
+
+
+@TRAINER_REGISTRY.register()
+class MaPLeFederated(TrainerX):
+    """The federated aggregator (trainers/maple_fed.py:24-500).
+
+    Process layout: launched with torch.distributed (WORLD_SIZE == FED.NUM_CLIENTS, backend nccl =
+    RCCL), rank r trains client r on its own GPU and FedAvg is an all-reduce; launched as one
+    process, the clients train one after another on one GPU, as in the reference."""
+
+    CLIENT_DATASETS = ("PatternNet", "Ucmerced", "EuroSAT")
+
+    def __init__(self, cfg):
+        self.lab2cname = {}
+        self.cfg = cfg
+        self.num_clients = cfg.FED.NUM_CLIENTS
+        self.num_rounds = cfg.FED.NUM_ROUNDS
+        self.local_epochs = cfg.FED.LOCAL_EPOCHS
+        self.clients: List[MaPLe] = []
+        self.global_weights = None
+        self.nan_stats = {"total_updates": 0, "failed_clients": [], "skipped_rounds": 0}
+        self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self.rank = dist.get_rank() if self.distributed else 0
+        if self.distributed and dist.get_world_size() != self.num_clients:
+            raise ValueError(f"WORLD_SIZE {dist.get_world_size()} != FED.NUM_CLIENTS {self.num_clients}: "
+                             "one client per rank")
+        super().__init__(cfg)
+
+    def _local_client_ids(self) -> List[int]:
+        return [self.rank] if self.distributed else list(range(self.num_clients))
+
+    def build_data_loader(self):
+        """trainers/maple_fed.py:48-159: the unified class list over the client datasets, then one data
+        manager per client (synthetic splits, see data.py)."""
+        if self.cfg.DATASET.ROOT and osp.isdir(self.cfg.DATASET.ROOT):
+            print(f"[INFO] DATASET.ROOT={self.cfg.DATASET.ROOT}: disk datasets are not wired on this path; "
+                  "using seeded synthetic client splits")
+        K = self.cfg.MODEL.NUM_CLASSES
+        names = unified_classnames(self.CLIENT_DATASETS, max(self.cfg.SEED, 0))
+        if K:
+            names = names[:K]
+        print(f"[INFO] Unified #classes = {len(names)}")
+        self.lab2cname = {i: c for i, c in enumerate(names)}
+        shots = self.cfg.DATASET.NUM_SHOTS if self.cfg.DATASET.NUM_SHOTS > 0 else 16
+        bs = self.cfg.DATALOADER.TRAIN_X.BATCH_SIZE
+        self.client_data_managers = {}
+        for i in self._local_client_ids():
+            self.client_data_managers[i] = SyntheticClientDataManager(
+                i, names, n_train=max(bs, min(shots * len(names), 64 * bs)), n_test=self.cfg.DATALOADER.TEST.BATCH_SIZE,
+                train_batch=bs, test_batch=self.cfg.DATALOADER.TEST.BATCH_SIZE, device=self.device,
+                seed=max(self.cfg.SEED, 0))
+        self.train_loader_x = self.val_loader = self.test_loader = self.dm = None
+
+    def build_model(self):
+        """trainers/maple_fed.py:164-176."""
+        global_classnames = list(self.lab2cname.values())
+        self.clients = []
+        for i in self._local_client_ids():
+            self.clients.append(MaPLe(self.cfg, client_id=i, classnames=global_classnames,
+                                      dm=self.client_data_managers[i], device=self.device))
+        c0 = self.clients[0]
+        self.register_model("MultiModalPromptLearner_Aggregator", c0.model, None, None)
+        self.fed = [FedAvgBucket(c.engine) for c in self.clients]
+        self.global_weights = self.clients[0].model.state_dict()
+
+    # ---------------------------------------------------------------- round loop
+    def train(self):
+        """trainers/maple_fed.py:228-303."""
+        for round_idx in range(self.num_rounds):
+            print(f"\n--- Federated Round {round_idx + 1}/{self.num_rounds} ---")
+            self.broadcast_weights()
+            round_losses, failed_local = [], []
+            for trainer, fed in zip(self.clients, self.fed):
+                print(f"[Client {trainer.client_id}] local training ...")
+                trainer.epoch = round_idx * self.local_epochs
+                trainer.max_epoch = (round_idx + 1) * self.local_epochs
+                last = 0.0
+                try:
+                    for ep in range(trainer.epoch, trainer.max_epoch):
+                        last = trainer.run_epoch(ep).get("avg_loss", 0.0)
+                    round_losses.append(last)
+                except RuntimeError as err:
+                    print(f"Client {trainer.client_id} failed training: {err}")
+                    self.nan_stats["failed_clients"].append(trainer.client_id)
+                    failed_local.append(trainer.client_id)
+                    fed.flag.fill_(1)   # excluded from the average
+            if round_losses:
+                print(f"[Round {round_idx + 1}] Avg local training loss = {sum(round_losses) / len(round_losses):.4f}")
+            n_valid = self._fedavg(failed_local)
+            if n_valid > 0:
+                self.nan_stats["total_updates"] += 1
+            else:
+                print("All clients failed! Reverting to previous global model.")
+                self.nan_stats["skipped_rounds"] += 1
+            self.global_weights = self.clients[0].model.state_dict()
+            if self.rank == 0:
+                res = self.clients[0].test()
+                print(f"[Round {round_idx + 1}] Test accuracy (client 0) = {res['accuracy']:.2f}%")
+        self.finalize_training()
+
+    def _fedavg(self, failed_local) -> int:
+        """check_weights_valid + safe_average_weights + broadcast, on the device (federated.py)."""
+        for c, fed in zip(self.clients, self.fed):
+            fed.start(collective=False)
+            if c.client_id in failed_local:
+                fed.flag.fill_(1)
+                fed.k.fedavg_pack(c.engine.flat16, c.engine.flat32, fed.flag, fed.buf)
+        if self.distributed:
+            dist.all_reduce(self.fed[0].buf, op=dist.ReduceOp.SUM)
+        else:
+            reduce_local(self.fed)
+        for fed in self.fed:
+            fed.finish()
+        return self.fed[0].n_valid()
+
+    # ---------------------------------------------------------------- reference utilities
+    def safe_average_weights(self, local_dicts, valid_clients=None):
+        """trainers/maple_fed.py:309-315 on state dicts (host API; the round loop averages on device)."""
+        avg = {}
+        for key in local_dicts[0].keys():
+            stacked = torch.stack([sd[key].float() for sd in local_dicts])
+            stacked = torch.nan_to_num(stacked, nan=0.0, posinf=1e4, neginf=-1e4)
+            avg[key] = torch.mean(stacked, dim=0).half()
+        return avg
+
+    def check_weights_valid(self, state_dict):
+        """trainers/maple_fed.py:317-325."""
+        for name, p in state_dict.items():
+            if torch.isnan(p).any():
+                print(f"NaN in {name}")
+                return False
+            if torch.isinf(p).any():
+                print(f"Inf in {name}")
+                return False
+        return True
+
+    def broadcast_weights(self, global_sd=None):
+        """trainers/maple_fed.py:327-339: load the global weights (already resident on every client after
+        the on-device FedAvg unless a state dict is given), drop SGD momentum, rebuild the scheduler
+        with last_epoch = epoch - 1."""
+        for c in self.clients:
+            if global_sd is not None:
+                c.model.load_state_dict(global_sd, strict=True)
+            c.engine.reset_momentum()
+            c.optim.rebuild(getattr(c, "epoch", None))
+            c.sched = c.optim.sched
+
+    def finalize_training(self):
+        print("\nTraining Summary:")
+        print(f"Completed Rounds: {self.nan_stats['total_updates']}")
+        print(f"Skipped Rounds: {self.nan_stats['skipped_rounds']}")
+        fail_rate = len(self.nan_stats["failed_clients"]) / max(1, self.num_clients)
+        print(f"Client Failure Rate: {fail_rate:.1%}")
+        if self.rank == 0:
+            result = self.clients[0].test()
+            print("Final test result:", result)
+            self.save_model()
+
+    def save_model(self, epoch=None, directory="", is_best=False, val_result=None):
+        """trainers/maple_fed.py:367-386: OUTPUT_DIR/MultiModalPromptLearner_Aggregator/model.pth.tar-<MAX_EPOCH>
+        with the fp16 global state dict (Dassl save_checkpoint format)."""
+        directory = directory or self.cfg.OUTPUT_DIR
+        target = osp.join(directory, "MultiModalPromptLearner_Aggregator")
+        os.makedirs(target, exist_ok=True)
+        sd = {k: v.detach().half().cpu() for k, v in self.clients[0].model.state_dict().items()}
+        ckpt = {"epoch": self.cfg.OPTIM.MAX_EPOCH, "state_dict": sd, "optimizer": None, "scheduler": None,
+                "val_result": val_result, "cfg": self.cfg.dump()}
+        fpath = osp.join(target, f"model.pth.tar-{self.cfg.OPTIM.MAX_EPOCH}")
+        torch.save(ckpt, fpath)
+        with open(osp.join(target, "checkpoint"), "w") as f:
+            f.write(osp.basename(fpath) + "\n")
+        if self.cfg.VERBOSE:
+            print(f"Model saved to {target}")
+        return fpath
+
+    def load_model(self, directory, epoch=None):
+        """trainers/maple_fed.py:388-411."""
+        if not directory:
+            print("Skipping load_model, no pretrained path given")
+            return
+        model_file = f"model.pth.tar-{epoch}" if epoch is not None else "model.pth.tar"
+        path = osp.join(directory, "MultiModalPromptLearner_Aggregator", model_file)
+        if not osp.exists(path):
+            raise FileNotFoundError(f"Model not found at {path}")
+        ckpt = torch.load(path, map_location="cpu", weights_only=True)
+        self.global_weights = ckpt["state_dict"]
+        print(f"Loaded aggregator weights from '{path}' (epoch={ckpt.get('epoch')}).")
+        if self.check_weights_valid(self.global_weights):
+            self.broadcast_weights(self.global_weights)
+            print("Broadcasted loaded global weights.")
+        else:
+            print("Warning: loaded global weights invalid! Skipping broadcast.")
+
+    def test(self):
+        """trainers/maple_fed.py:493-498: evaluate the global model on client 0."""
+        if self.rank != 0:
+            return {}
+        return self.clients[0].test(evaluate_train=True)

@@ -93,6 +93,10 @@ int mf_clip_loss_fwd_bwd(const void* img, const void* txt, const void* img_n, co
                          void* dmm, float* cos_ws, float* loss_out, void* dimg_n, void* dtxt_n, void* dimg,
                          void* dtxt, void* stream);
 
+/* eval predictions (trainers/maple.py:674-677): pred[b] = argmax_k logits (first max; NaN is the max);
+ * acc[0] += #correct, acc[1] += B (device-side accuracy counters, read once per test pass)           */
+int mf_argmax_correct(const void* logits, int B, int K, const int64_t* label, int64_t* pred, float* acc, void* stream);
+
 /* ---- optimizer / federated averaging (trainers/maple.py:592-598; trainers/maple_fed.py:309-325) */
 int mf_optim_chunk_bytes(void);
 int mf_optim_chunk_elems(void);

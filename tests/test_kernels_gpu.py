@@ -355,3 +355,19 @@ def test_fedavg_kernels_single_client(dev):
     e.flat32[5] = float("nan")
     assert fed.run() == 0
     assert torch.equal(e.flat32, new32) and torch.equal(e.flat16, g16)
+
+
+def test_argmax_correct(dev):
+    torch.manual_seed(9)
+    B, K = 100, 38
+    logits = torch.randn(B, K, device=dev).half()
+    logits[3, 5] = logits[3, 7] = 50.0          # tie: first index wins
+    logits[4, 9] = float("nan")                 # NaN is the maximum (torch.argmax)
+    label = torch.randint(0, K, (B,), device=dev)
+    label[:10] = logits[:10].float().argmax(1)
+    pred = torch.empty(B, dtype=torch.int64, device=dev)
+    acc = torch.zeros(2, device=dev)
+    ops.argmax_correct(logits, label, pred, acc)
+    ref = logits.float().cpu().argmax(1)
+    assert torch.equal(pred.cpu(), ref)
+    assert acc[0].item() == (ref == label.cpu()).sum().item() and acc[1].item() == B
