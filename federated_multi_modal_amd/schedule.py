@@ -15,6 +15,8 @@ SGD kernel through the engine's hyper-parameter buffer.
 """
 from __future__ import annotations
 
+import warnings
+
 import torch
 from torch.optim.lr_scheduler import CosineAnnealingLR, _LRScheduler
 
@@ -87,6 +89,10 @@ def build_lr_scheduler(optimizer, optim_cfg):
         else:
             raise ValueError(f"Unknown warmup type: {optim_cfg.WARMUP_TYPE}")
     return sched
+
+
+# the dummy optimizer never steps (the SGD runs on the device), which torch would warn about
+warnings.filterwarnings("ignore", message="Detected call of `lr_scheduler.step\\(\\)` before")
 
 
 class HostLR:
