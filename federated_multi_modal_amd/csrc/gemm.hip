@@ -38,7 +38,55 @@ struct GemmArgs {
   f16* aux_out;
   int64_t lda, ldb, ldc, ld_aux;
   int M, N, K;
+  int vec8;  // C / aux row strides are multiples of 8 elements -> 16-byte epilogue accesses
 };
+
+// Elementwise epilogue on 8 consecutive columns (fp16 staged value t = the GEMM result rounded at
+// the reference's first rounding point: fp16(acc + bias) or fp16(acc)).
+template <int EPI>
+MF_DEV void epi8(const GemmArgs& g, int64_t m, int n, int cnt, const f16* t) {
+  f16* crow = (f16*)g.C + m * g.ldc + n;
+  if (cnt == 8 && g.vec8) {
+    f16x8 tv = *(const f16x8*)t;
+    f16x8 out;
+    if constexpr (EPI == EPI_NONE || EPI == EPI_BIAS) {
+      out = tv;
+    } else if constexpr (EPI == EPI_BIAS_RESID || EPI == EPI_RESID) {
+      f16x8 rr = *(const f16x8*)(g.aux_in + m * g.ld_aux + n);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out[e] = (f16)((float)rr[e] + (float)tv[e]);
+    } else if constexpr (EPI == EPI_BIAS_GELU) {
+      *(f16x8*)(g.aux_out + m * g.ld_aux + n) = tv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float t2;
+        out[e] = (f16)quick_gelu16((float)tv[e], &t2);
+      }
+    } else if constexpr (EPI == EPI_DGELU) {
+      f16x8 ff = *(const f16x8*)(g.aux_in + m * g.ld_aux + n);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out[e] = (f16)quick_gelu16_bwd((float)tv[e], (float)ff[e]);
+    }
+    *(f16x8*)crow = out;
+    return;
+  }
+  for (int e = 0; e < cnt; ++e) {
+    const float tvv = (float)t[e];
+    float o;
+    if constexpr (EPI == EPI_NONE || EPI == EPI_BIAS) {
+      o = tvv;
+    } else if constexpr (EPI == EPI_BIAS_RESID || EPI == EPI_RESID) {
+      o = (float)g.aux_in[m * g.ld_aux + n + e] + tvv;
+    } else if constexpr (EPI == EPI_BIAS_GELU) {
+      float t2;
+      g.aux_out[m * g.ld_aux + n + e] = (f16)tvv;
+      o = quick_gelu16(tvv, &t2);
+    } else if constexpr (EPI == EPI_DGELU) {
+      o = quick_gelu16_bwd(tvv, (float)g.aux_in[m * g.ld_aux + n + e]);
+    }
+    crow[e] = (f16)o;
+  }
+}
 
 constexpr int BK = 64;
 
@@ -70,7 +118,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g) {
   constexpr int B_INS = BN / 8 / NW;
   static_assert(A_INS * 8 * NW == BM && B_INS * 8 * NW == BN, "tile / wave split");
   constexpr int STAGE = (BM + BN) * BK;  // fp16 elements per stage
-  __shared__ __attribute__((aligned(1024))) f16 lds[S * STAGE];
+  constexpr int LDS_ELEMS = S * STAGE > BM * (BN + 8) ? S * STAGE : BM * (BN + 8);
+  __shared__ __attribute__((aligned(1024))) f16 lds[LDS_ELEMS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -171,53 +220,56 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g) {
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   }
 
-  // epilogue: lane holds C[m = .. + fr][n = .. + 4*fg + e], e = 0..3
+  // epilogue.  lane holds C[m = .. + fr][n = .. + 4*fg + e], e = 0..3.
+  if constexpr (EPI == EPI_F32) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wave_m * WTM + i * 16 + fr;
-    if (m >= g.M) continue;
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wave_m * WTM + i * 16 + fr;
+      if (m >= g.M) continue;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wave_n * WTN + j * 16 + 4 * fg;
-      if (n >= g.N) continue;
-      f32x4 v = acc[i][j];
-      if constexpr (EPI == EPI_F32) {
-        *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = v;
-      } else {
-        f16x4 out;
-        if constexpr (EPI == EPI_NONE) {
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wave_n * WTN + j * 16 + 4 * fg;
+        if (n < g.N) *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = acc[i][j];
+      }
+    }
+  } else {
+    // 1) the first fp16 rounding point in registers (fp16(acc + bias) / fp16(acc)), staged through LDS
+    //    as a [BM][BN+8] fp16 tile; 2) the whole workgroup streams rows out with 16-byte accesses
+    //    (full cache lines) applying the rest of the epilogue (residual, QuickGELU, QuickGELU').
+    constexpr int LDC = BN + 8;
+    f16* sC = lds;
+    __syncthreads();  // every wave is done with the operand ring
 #pragma unroll
-          for (int e = 0; e < 4; ++e) out[e] = (f16)v[e];
-        } else if constexpr (EPI == EPI_BIAS) {
+    for (int i = 0; i < TM; ++i) {
+      const int ml = wave_m * WTM + i * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nl = wave_n * WTN + j * 16 + 4 * fg;
+        f32x4 v = acc[i][j];
+        f16x4 t;
+        if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU) {
+          const int n = min(n0 + nl, g.N - 4);
           f16x4 b = *(const f16x4*)(g.bias + n);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) out[e] = (f16)(v[e] + (float)b[e]);
-        } else if constexpr (EPI == EPI_BIAS_RESID) {
-          f16x4 b = *(const f16x4*)(g.bias + n);
-          f16x4 rr = *(const f16x4*)(g.aux_in + (int64_t)m * g.ld_aux + n);
+          for (int e = 0; e < 4; ++e) t[e] = (f16)(v[e] + (float)b[e]);
+        } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) out[e] = (f16)((float)rr[e] + r16(v[e] + (float)b[e]));
-        } else if constexpr (EPI == EPI_RESID) {
-          f16x4 rr = *(const f16x4*)(g.aux_in + (int64_t)m * g.ld_aux + n);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) out[e] = (f16)((float)rr[e] + r16(v[e]));
-        } else if constexpr (EPI == EPI_BIAS_GELU) {
-          f16x4 b = *(const f16x4*)(g.bias + n);
-          f16x4 fo;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float f = r16(v[e] + (float)b[e]);
-            float t2;
-            fo[e] = (f16)f;
-            out[e] = (f16)quick_gelu16(f, &t2);
-          }
-          *(f16x4*)(g.aux_out + (int64_t)m * g.ld_aux + n) = fo;
-        } else if constexpr (EPI == EPI_DGELU) {
-          f16x4 ff = *(const f16x4*)(g.aux_in + (int64_t)m * g.ld_aux + n);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) out[e] = (f16)quick_gelu16_bwd(r16(v[e]), (float)ff[e]);
+          for (int e = 0; e < 4; ++e) t[e] = (f16)v[e];
         }
-        *(f16x4*)((f16*)g.C + (int64_t)m * g.ldc + n) = out;
+        *(f16x4*)(sC + ml * LDC + nl) = t;
+      }
+    }
+    __syncthreads();
+    constexpr int CPR = BN / 8;        // 16-byte chunks per tile row
+    constexpr int RPP = NT / CPR;      // rows per pass
+    const int c8 = tid % CPR;
+    const int n = n0 + 8 * c8;
+    const int cnt = min(8, g.N - n);
+    if (cnt > 0) {
+#pragma unroll 4
+      for (int r = tid / CPR; r < BM; r += RPP) {
+        const int m = m0 + r;
+        if (m < g.M) epi8<EPI>(g, m, n, cnt, sC + r * LDC + 8 * c8);
       }
     }
   }
@@ -254,8 +306,10 @@ extern "C" int mf_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb
   if ((epilogue == EPI_BIAS_RESID || epilogue == EPI_DGELU || epilogue == EPI_RESID) && !aux_in)
     return mf_set_error("mf_gemm_nt: epilogue needs aux_in", -1);
   if (epilogue == EPI_BIAS_GELU && !aux_out) return mf_set_error("mf_gemm_nt: epilogue needs aux_out", -1);
+  const int vec8 = (ldc % 8 == 0) && (ld_aux % 8 == 0) && ((uintptr_t)C % 16 == 0) &&
+                   (!aux_in || (uintptr_t)aux_in % 16 == 0) && (!aux_out || (uintptr_t)aux_out % 16 == 0);
   GemmArgs a{(const f16*)A, (const f16*)B, C, (const f16*)bias, (const f16*)aux_in, (f16*)aux_out,
-             lda, ldb, ldc, ld_aux, M, N, K};
+             lda, ldb, ldc, ld_aux, M, N, K, vec8};
   hipStream_t st = (hipStream_t)stream;
   if (tile == 0) {  // heuristic: fill the 256 CUs
     int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
