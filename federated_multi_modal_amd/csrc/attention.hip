@@ -18,6 +18,9 @@
 //   bwd:  dK/dV kernel (grid over 64-key blocks, Q and dO for the head in LDS) and dQ kernel
 //         (grid over 64-query blocks, K and V in LDS); P is recomputed from the saved LSE.
 // LDS images are [rows][64] fp16 with the 16-byte chunk XOR swizzle chunk ^ (row & 7).
+#include <algorithm>
+#include <cstdlib>
+
 #include "mf_common.h"
 
 namespace {
@@ -45,22 +48,32 @@ MF_DEV f16x8 ld_frag(const f16* img, int row, int chunk) {
 }
 
 // Stage rows [0, LP) of one head (column offset col0 inside the qkv-like row) into a swizzled
-// LDS image; rows >= L are zero.
+// [LP][64] LDS image by global_load_lds (16 B per lane, no VGPR round trip; all of a block's
+// loads are in flight together and retired by one wait).  The LDS side of an LDS-DMA is
+// lane-linear (8 rows x 128 B per wave instruction), so the chunk XOR swizzle is applied to the
+// per-lane SOURCE address.  Rows >= L re-read row L-1 (finite data; the kernels mask them).
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 template <int LP>
 MF_DEV void stage_rows(f16* img, const f16* base, int64_t ld, int L, int col0) {
-  for (int idx = threadIdx.x; idx < LP * 8; idx += blockDim.x) {
-    const int row = idx >> 3, c = idx & 7;
-    f16x8 v = {};
-    if (row < L) v = *(const f16x8*)(base + (int64_t)row * ld + col0 + c * 8);
-    *(f16x8*)(img + row * 64 + ((c ^ (row & 7)) << 3)) = v;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lrow = lane >> 3, lchunk = (lane & 7) ^ lrow;
+  for (int i = w; i < LP / 8; i += nw) {
+    int row = i * 8 + lrow;
+    row = row < L ? row : L - 1;
+    __builtin_amdgcn_global_load_lds((const void*)(base + (int64_t)row * ld + col0 + lchunk * 8),
+                                     (lds_ptr_t)(img + i * 8 * 64), 16, 0, 0);
   }
+}
+MF_DEV void stage_wait() {
+  __builtin_amdgcn_s_waitcnt((0 & 15) | (7 << 4) | (15 << 8));  // vmcnt(0): this wave's LDS-DMA landed
+  __syncthreads();                                              // ... and every other wave's
 }
 
 constexpr float kScale = 0.125f;  // 1/sqrt(64), SDPA default
 
 // ---------------------------------------------------------------------------------------------
 template <int LKP, bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
+__global__ __launch_bounds__(512, 4) void attn_fwd_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
                                                       f16* __restrict__ out, int64_t ld_out,
                                                       float* __restrict__ lse, int ld_lse, int L, int H) {
   constexpr int NKT = LKP / 16;
@@ -71,11 +84,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const f16* __restrict__ q
   const f16* base = qkv + (int64_t)n * L * ld_qkv;
   stage_rows<LKP>(sK, base, ld_qkv, L, D + h * 64);
   stage_rows<LKP>(sV, base, ld_qkv, L, 2 * D + h * 64);
-  __syncthreads();
+  stage_wait();
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int q0 = blockIdx.y * 64 + w * 16;
-  if (q0 >= L) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // every wave takes 16-row tiles w, w + nw, ... of this head (the staged operands are shared)
+  for (int q0 = (blockIdx.y * nw + w) * 16; q0 < L; q0 += gridDim.y * nw * 16) {
   const int fr = lane & 15, fg = lane >> 4;
   const int q = q0 + fr;
   const int qc = q < L ? q : L - 1;
@@ -83,58 +96,85 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const f16* __restrict__ q
 #pragma unroll
   for (int s = 0; s < 2; ++s) qf[s] = *(const f16x8*)(base + (int64_t)qc * ld_qkv + h * 64 + 32 * s + 8 * fg);
 
+  // two passes over the keys, 32 at a time, so that no score array lives in registers:
+  //   1) raw S = K Q^T -> row max;  2) S again, P = exp((S - max) / 8) (fp32), l = sum P,
+  //   O += V^T fp16(P)  (the reference's single-block CPU flash kernel: P relative to the final row
+  //   max; the 1/8 scale and log2(e) are folded into one FMA before v_exp_f32).
+  // LDS offsets: 32*ks is a multiple of 8, so the chunk swizzle depends on the lane only and a key
+  // block just adds ks * 32 rows * 64 elements.
+  const int ii = lane & 15;
+  int koff[2][2], voff[4][2];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int row = 16 * hf + fr;
+      koff[s2][hf] = row * 64 + (((4 * s2 + fg) ^ (row & 7)) << 3);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) voff[dt][hf] = sw_off(16 * hf + 4 * fg + (ii >> 2), 16 * dt + 4 * (ii & 3));
+  }
   const int kt_end = CAUSAL ? min(NKT, (q0 + 16 + 15) / 16) : NKT;
-  f32x4 sacc[NKT];
-  float m = -INFINITY;
+  const int ks_end = (kt_end + 1) / 2;
+  auto scores = [&](int ks, f32x4& a0, f32x4& a1) {
+    a0 = (f32x4){0.f, 0.f, 0.f, 0.f};
+    a1 = a0;
+    const f16* kb = sK + ks * 32 * 64;
 #pragma unroll
-  for (int kt = 0; kt < NKT; ++kt) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (kt < kt_end) {
+    for (int s2 = 0; s2 < 2; ++s2) {
+      a0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[s2][0]), qf[s2], a0, 0, 0, 0);
+      a1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[s2][1]), qf[s2], a1, 0, 0, 0);
+    }
+    if (CAUSAL || 32 * ks + 32 > L) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        f16x8 kf = ld_frag(sK, kt * 16 + fr, 4 * s + fg);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[s], acc, 0, 0, 0);
+      for (int i = 0; i < 4; ++i) {
+        const int key0 = 32 * ks + 4 * fg + i, key1 = key0 + 16;
+        if (key0 >= L || (CAUSAL && key0 > q)) a0[i] = -INFINITY;
+        if (key1 >= L || (CAUSAL && key1 > q) || 2 * ks + 1 >= kt_end) a1[i] = -INFINITY;
       }
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int key = kt * 16 + 4 * fg + i;
-      float v = acc[i] * kScale;
-      if (key >= L || (CAUSAL && key > q) || kt >= kt_end) v = -INFINITY;
-      acc[i] = v;
-      m = fmaxf(m, v);
-    }
-    sacc[kt] = acc;
+  };
+  float m = -INFINITY;
+#pragma unroll 1
+  for (int ks = 0; ks < ks_end; ++ks) {
+    f32x4 a0, a1;
+    scores(ks, a0, a1);
+    m = fmaxf(m, fmaxf(fmaxf(a0[0], a0[1]), fmaxf(a0[2], a0[3])));
+    m = fmaxf(m, fmaxf(fmaxf(a1[0], a1[1]), fmaxf(a1[2], a1[3])));
   }
   m = fmaxf(m, __shfl_xor(m, 16, 64));
   m = fmaxf(m, __shfl_xor(m, 32, 64));
+  constexpr float kLog2eScale = 0.125f * 1.4426950408889634f;
+  const float mb = -m * kLog2eScale;
   float l = 0.f;
-#pragma unroll
-  for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float p = __expf(sacc[kt][i] - m);
-      sacc[kt][i] = p;
-      l += p;
-    }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-
   f32x4 oacc[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) oacc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int ks = 0; ks < ks_end; ++ks) {
+    f32x4 a0, a1;
+    scores(ks, a0, a1);
+    f16x8 pf;
 #pragma unroll
-  for (int ks = 0; ks < NKT / 2; ++ks) {
-    if (CAUSAL && 2 * ks >= kt_end) break;
-    f16x8 pf = {(f16)sacc[2 * ks][0], (f16)sacc[2 * ks][1], (f16)sacc[2 * ks][2], (f16)sacc[2 * ks][3],
-                (f16)sacc[2 * ks + 1][0], (f16)sacc[2 * ks + 1][1], (f16)sacc[2 * ks + 1][2],
-                (f16)sacc[2 * ks + 1][3]};
+    for (int i = 0; i < 4; ++i) {
+      const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(a0[i], kLog2eScale, mb));
+      const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(a1[i], kLog2eScale, mb));
+      l += p0 + p1;
+      pf[i] = (f16)p0;
+      pf[4 + i] = (f16)p1;
+    }
+    const f16* vb = sV + ks * 32 * 64;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      f16x8 vf = cat8(tr_read(sV, 32 * ks + 4 * fg, 16 * dt, lane), tr_read(sV, 32 * ks + 16 + 4 * fg, 16 * dt, lane));
+      s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[dt][0]));
+      s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[dt][1]));
+      f16x8 vf = cat8(__builtin_bit_cast(f16x4, v0), __builtin_bit_cast(f16x4, v1));
       oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf, oacc[dt], 0, 0, 0);
     }
   }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  m *= kScale;  // the scaled row max (for the LSE the backward recomputes P from)
   if (q < L) {
     const float inv = 1.0f / l;
     f16* orow = out + ((int64_t)n * L + q) * ld_out + h * 64;
@@ -146,6 +186,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const f16* __restrict__ q
       *(f16x4*)(orow + 16 * dt + 4 * fg) = o;
     }
     if (fg == 0) lse[(int64_t)nh * ld_lse + q] = m + __logf(l);
+  }
   }
 }
 
@@ -171,7 +212,7 @@ __global__ void attn_bwd_dot_kernel(const f16* __restrict__ out, int64_t ld_out,
 
 // dK, dV: one workgroup per (n, h, 64-key block); each wave 16 keys, loops over all queries ----
 template <int LQP, bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
+__global__ __launch_bounds__(512, 4) void attn_bwd_dkv_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
                                                           const f16* __restrict__ dout, int64_t ld_dout,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ dq_dot, int ld_lse,
@@ -189,11 +230,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const f16* __restrict
     sL[i] = i < L ? lse[(int64_t)nh * ld_lse + i] : INFINITY;
     sD[i] = i < L ? dq_dot[(int64_t)nh * ld_lse + i] : 0.f;
   }
-  __syncthreads();
+  stage_wait();
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int k0 = blockIdx.y * 64 + w * 16;
-  if (k0 >= L) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // every wave takes 16-row tiles w, w + nw, ... of this head (the staged operands are shared)
+  for (int k0 = (blockIdx.y * nw + w) * 16; k0 < L; k0 += gridDim.y * nw * 16) {
   const int fr = lane & 15, fg = lane >> 4;
   const int key = k0 + fr;
   const int kc = key < L ? key : L - 1;
@@ -207,6 +248,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const f16* __restrict
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dv[dt] = dk[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+#pragma unroll 1
   for (int qp = 0; qp < LQP / 32; ++qp) {
     if (CAUSAL && 32 * qp + 31 < k0) continue;  // every query < every key of this wave
     f16x8 pf, dsf;
@@ -253,11 +295,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const f16* __restrict
       *(f16x4*)(row + 2 * D + 16 * dt + 4 * fg) = ov;
     }
   }
+  }
 }
 
 // dQ: one workgroup per (n, h, 64-query block); each wave 16 queries, loops over all keys -------
 template <int LKP, bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
+__global__ __launch_bounds__(512, 4) void attn_bwd_dq_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
                                                          const f16* __restrict__ dout, int64_t ld_dout,
                                                          const float* __restrict__ lse,
                                                          const float* __restrict__ dq_dot, int ld_lse,
@@ -270,11 +313,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const f16* __restrict_
   const f16* base = qkv + (int64_t)n * L * ld_qkv;
   stage_rows<LKP>(sK, base, ld_qkv, L, D + h * 64);
   stage_rows<LKP>(sV, base, ld_qkv, L, 2 * D + h * 64);
-  __syncthreads();
+  stage_wait();
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int q0 = blockIdx.y * 64 + w * 16;
-  if (q0 >= L) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // every wave takes 16-row tiles w, w + nw, ... of this head (the staged operands are shared)
+  for (int q0 = (blockIdx.y * nw + w) * 16; q0 < L; q0 += gridDim.y * nw * 16) {
   const int fr = lane & 15, fg = lane >> 4;
   const int q = q0 + fr;
   const int qc = q < L ? q : L - 1;
@@ -289,7 +332,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const f16* __restrict_
   f32x4 dq[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dq[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
+#pragma unroll 1
   for (int ks = 0; ks < NKT / 2; ++ks) {
     if (CAUSAL && 32 * ks > q0 + 15) break;
     f16x8 dsf;
@@ -328,6 +371,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const f16* __restrict_
       *(f16x4*)(row + 16 * dt + 4 * fg) = o;
     }
   }
+  }
 }
 
 #define MF_ATTN_DISPATCH(LP, CALL)                         \
@@ -344,6 +388,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const f16* __restrict_
   }
 
 inline int padded_len(int L) { return ((L + 31) / 32) * 32; }
+// one workgroup per (sequence, head): up to 8 waves sharing the staged operands, one 16-row tile each
+inline int attn_threads(int L) {
+  static const int maxw = getenv("MAPFED_ATTN_WAVES") ? atoi(getenv("MAPFED_ATTN_WAVES")) : 8;  // tuning knob
+  return 64 * std::max(1, std::min(maxw, (L + 15) / 16));
+}
+// query-tile split of a head over workgroups: enough workgroups to cover the chip (measured best:
+// 2 at N*H = 384, 4 at N*H = 48; tests/diagnostics/attn_bench.py), at the cost of re-staging K/V
+inline int attn_qsplit(int NH, int L) {
+  static const int qs = getenv("MAPFED_ATTN_QSPLIT") ? atoi(getenv("MAPFED_ATTN_QSPLIT")) : 0;  // tuning knob
+  const int want = qs > 0 ? qs : std::min(4, (768 + NH - 1) / NH);
+  return std::max(1, std::min(want, (L + 15) / 16 / 2));
+}
 
 }  // namespace
 
@@ -353,13 +409,13 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
   if (L <= 0 || L > 256) return mf_set_error("mf_attention_fwd: 0 < L <= 256 required", -1);
   if (ld_lse < L || (ld_qkv % 8) || (ld_out % 4)) return mf_set_error("mf_attention_fwd: bad strides", -1);
   const int LP = padded_len(L);
-  dim3 grid(N * H, (L + 63) / 64);
+  const dim3 grid(N * H, attn_qsplit(N * H, L)), block(attn_threads(L));
   hipStream_t st = (hipStream_t)stream;
 #define CALLF(P)                                                                                            \
   if (causal)                                                                                               \
-    attn_fwd_kernel<P, true><<<grid, 256, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); \
+    attn_fwd_kernel<P, true><<<grid, block, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); \
   else                                                                                                      \
-    attn_fwd_kernel<P, false><<<grid, 256, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H);
+    attn_fwd_kernel<P, false><<<grid, block, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H);
   MF_ATTN_DISPATCH(LP, CALLF)
 #undef CALLF
   MF_CHECK_LAUNCH();
@@ -378,17 +434,17 @@ extern "C" int mf_attention_bwd(const void* qkv, int64_t ld_qkv, const void* out
   attn_bwd_dot_kernel<<<(tot + 255) / 256, 256, 0, st>>>((const f16*)out, ld_out, (const f16*)dout, ld_dout,
                                                         dq_dot_ws, ld_lse, N, L, H);
   MF_CHECK_LAUNCH();
-  dim3 grid(N * H, (L + 63) / 64);
+  const dim3 grid(N * H, attn_qsplit(N * H, L)), block(attn_threads(L));
 #define CALLB(P)                                                                                                 \
   if (causal) {                                                                                                  \
-    attn_bwd_dkv_kernel<P, true><<<grid, 256, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)dout, ld_dout, lse,    \
+    attn_bwd_dkv_kernel<P, true><<<grid, block, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)dout, ld_dout, lse,    \
                                                        dq_dot_ws, ld_lse, (f16*)dqkv, ld_dqkv, L, H);              \
-    attn_bwd_dq_kernel<P, true><<<grid, 256, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)dout, ld_dout, lse,     \
+    attn_bwd_dq_kernel<P, true><<<grid, block, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)dout, ld_dout, lse,     \
                                                       dq_dot_ws, ld_lse, (f16*)dqkv, ld_dqkv, L, H);               \
   } else {                                                                                                       \
-    attn_bwd_dkv_kernel<P, false><<<grid, 256, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)dout, ld_dout, lse,   \
+    attn_bwd_dkv_kernel<P, false><<<grid, block, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)dout, ld_dout, lse,   \
                                                         dq_dot_ws, ld_lse, (f16*)dqkv, ld_dqkv, L, H);             \
-    attn_bwd_dq_kernel<P, false><<<grid, 256, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)dout, ld_dout, lse,    \
+    attn_bwd_dq_kernel<P, false><<<grid, block, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)dout, ld_dout, lse,    \
                                                        dq_dot_ws, ld_lse, (f16*)dqkv, ld_dqkv, L, H);              \
   }
   MF_ATTN_DISPATCH(LP, CALLB)
