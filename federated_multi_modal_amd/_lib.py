@@ -20,6 +20,8 @@ SIGNATURES = {
     "mf_layernorm_fwd": [P, L, P, P, P, P, L, P, P, I, I, P],
     "mf_layernorm_bwd_blocks": [I],
     "mf_layernorm_bwd": [P, L, P, L, P, P, P, P, P, L, P, L, P, P, P, I, I, I, P],
+    "mf_col_reduce_desc_bytes": [],
+    "mf_col_reduce_batch": [P, I, I, P],
     "mf_attention_fwd": [P, L, P, L, P, I, I, I, I, I, P],
     "mf_attention_bwd": [P, L, P, L, P, L, P, P, I, P, L, I, I, I, I, P],
     "mf_im2col_patch": [P, I, P, I, I, I, P],
@@ -46,7 +48,7 @@ SIGNATURES = {
 }
 # functions that return a value, not a status
 _VALUE_FUNCS = {"mf_abi_version", "mf_layernorm_bwd_blocks", "mf_colsum_blocks", "mf_optim_chunk_bytes",
-                "mf_optim_chunk_elems"}
+                "mf_optim_chunk_elems", "mf_col_reduce_desc_bytes"}
 
 _LIB = None
 

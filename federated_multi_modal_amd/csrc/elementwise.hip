@@ -98,26 +98,47 @@ __global__ void inject_kernel(f16* __restrict__ x, const float* __restrict__ pro
   x[((int64_t)n * L + row0 + r) * D + d] = (f16)prompt[r * D + d];
 }
 
-// out[r, d] (=|+=) sum_n dx[n*L + row0 + r, d]  (fp32 accumulation, fixed n order), then the
+// out[r, d] (=|+=) sum_n dx[n*L + row0 + r, d]  (fp32 accumulation in a fixed order), then the
 // injected rows of dx are zeroed (the previous layer's outputs there were discarded).
 // out_f16: round once to fp16 (fp16 source tensors, e.g. ctx / shared_ctx); else fp32.
-__global__ void inject_bwd_kernel(f16* __restrict__ dx, int N, int L, int row0, int nrows, int D, void* out,
-                                  int out_f16, int accumulate, int zero_rows) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nrows * D) return;
-  const int d = t % D, r = t / D;
-  float s = 0.f;
-  for (int n = 0; n < N; ++n) {
-    f16* p = dx + ((int64_t)n * L + row0 + r) * D + d;
-    s += (float)*p;
-    if (zero_rows) *p = (f16)0.f;
+// grid (ceil(D/256), nrows), 1024 threads: lane -> 4 consecutive columns, 16 wave groups split the
+// batch (n = g, g+16, ...), partials combined through LDS in group order.
+__global__ __launch_bounds__(1024) void inject_bwd_kernel(f16* __restrict__ dx, int N, int L, int row0, int nrows,
+                                                          int D, void* out, int out_f16, int accumulate,
+                                                          int zero_rows) {
+  __shared__ f32x4 red[16][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int r = blockIdx.y;
+  const int d = blockIdx.x * 256 + lane * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (d < D) {
+    for (int n = g; n < N; n += 16) {
+      f16x4* p = (f16x4*)(dx + ((int64_t)n * L + row0 + r) * D + d);
+      const f16x4 v = *p;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[e] += (float)v[e];
+      if (zero_rows) *p = (f16x4){(f16)0.f, (f16)0.f, (f16)0.f, (f16)0.f};
+    }
   }
-  if (out_f16) {
-    f16* o = (f16*)out + t;
-    *o = accumulate ? (f16)((float)*o + r16(s)) : (f16)s;
-  } else {
-    float* o = (float*)out + t;
-    *o = accumulate ? *o + s : s;
+  red[g][lane] = s;
+  __syncthreads();
+  if (g == 0 && d < D) {
+    f32x4 t = red[0][lane];
+#pragma unroll
+    for (int k = 1; k < 16; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[e] += red[k][lane][e];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = r * D + d + e;
+      if (out_f16) {
+        f16* o = (f16*)out + i;
+        *o = accumulate ? (f16)((float)*o + r16(t[e])) : (f16)t[e];
+      } else {
+        float* o = (float*)out + i;
+        *o = accumulate ? *o + t[e] : t[e];
+      }
+    }
   }
 }
 
@@ -290,8 +311,10 @@ extern "C" int mf_prompt_inject_fwd(void* x, const float* prompt, int N, int L, 
 extern "C" int mf_prompt_inject_bwd(void* dx, int N, int L, int row0, int nrows, int D, void* out, int out_f16,
                                     int accumulate, int zero_rows, void* stream) {
   if (row0 < 0 || row0 + nrows > L) return mf_set_error("mf_prompt_inject_bwd: rows out of range", -1);
-  inject_bwd_kernel<<<nblk((int64_t)nrows * D), 256, 0, (hipStream_t)stream>>>((f16*)dx, N, L, row0, nrows, D, out,
-                                                                               out_f16, accumulate, zero_rows);
+  if (D % 4) return mf_set_error("mf_prompt_inject_bwd: D % 4", -1);
+  inject_bwd_kernel<<<dim3((D + 255) / 256, nrows), 1024, 0, (hipStream_t)stream>>>((f16*)dx, N, L, row0, nrows, D,
+                                                                                    out, out_f16, accumulate,
+                                                                                    zero_rows);
   MF_CHECK_LAUNCH();
   return 0;
 }

@@ -205,8 +205,55 @@ extern "C" int mf_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int
     ln_bwd_kernel<512><<<nblk, 256, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, row_index, gamma, mean, rstd,
                                              (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows);
   MF_CHECK_LAUNCH();
+  if (!dgamma && !dbeta) return 0;  // partials only: the caller reduces them later (mf_col_reduce_batch)
+  if (!dgamma || !dbeta) return mf_set_error("mf_layernorm_bwd: dgamma and dbeta go together", -1);
   col_reduce_kernel<false><<<dim3((D + 63) / 64, 2), 1024, 0, st>>>(dg_part, db_part, nblk, D, D, dgamma, dbeta,
                                                                     accumulate);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- batched deferred column reductions (every LayerNorm's dgamma/dbeta of a backward pass in one launch)
+namespace {
+struct ColReduceDesc {
+  const float* part;  // [nblk][C] partial sums
+  float* out;         // [C]
+  int nblk, C, accumulate, pad;
+};
+__global__ __launch_bounds__(1024) void col_reduce_batch_kernel(const ColReduceDesc* __restrict__ descs) {
+  __shared__ float red[16][65];
+  const ColReduceDesc d = descs[blockIdx.y];
+  if ((int)blockIdx.x * 64 >= d.C) return;
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < d.C) {
+    int b = g;
+    for (; b + 48 < d.nblk; b += 64) {
+      s0 += d.part[(int64_t)b * d.C + c];
+      s1 += d.part[(int64_t)(b + 16) * d.C + c];
+      s2 += d.part[(int64_t)(b + 32) * d.C + c];
+      s3 += d.part[(int64_t)(b + 48) * d.C + c];
+    }
+    for (; b < d.nblk; b += 16) s0 += d.part[(int64_t)b * d.C + c];
+  }
+  red[g][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (g == 0 && c < d.C) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][lane];
+    d.out[c] = d.accumulate ? d.out[c] + s : s;
+  }
+}
+}  // namespace
+
+extern "C" int mf_col_reduce_desc_bytes(void) { return (int)sizeof(ColReduceDesc); }
+
+extern "C" int mf_col_reduce_batch(const void* descs, int n, int max_cols, void* stream) {
+  if (n <= 0) return 0;
+  col_reduce_batch_kernel<<<dim3((max_cols + 63) / 64, n), 1024, 0, (hipStream_t)stream>>>(
+      (const ColReduceDesc*)descs);
   MF_CHECK_LAUNCH();
   return 0;
 }

@@ -178,7 +178,6 @@ class _Tower:
         self.dQKV = e(R, 3 * D)
         self.dF = e(R, 4 * D)
         self.attn_ws = e(N * H * L, dt=F32)
-        self.ln_ws = e(ops.layernorm_ws_floats(R, D), dt=F32)
         self.cs_ws = e(ops.colsum_ws_floats(R, 4 * D), dt=F32)
         # transposed operands of the block-11 weight gradients (zero padded to Rp columns)
         self.tA = torch.zeros(4 * D, self.Rp, device=dev, dtype=F16)
@@ -242,8 +241,8 @@ class _Tower:
             ops.gemm_nt(self.dF, self.wt(i, "mlp.c_fc.weight"), self.dH, epilogue=ops.EPI_NONE)
             if trainable_w:
                 self._dw(self.dF, self.H2, self.g(i, "mlp.c_fc.weight"), self.g(i, "mlp.c_fc.bias"))
-            ops.layernorm_bwd(self.dH, self.X1[i], self.p(i, "ln_2.weight"), self.mean2[i], self.rstd2[i], dX,
-                              self.g(i, "ln_2.weight"), self.g(i, "ln_2.bias"), self.ln_ws, dres=dX)
+            self.e.lnb.bwd(self.dH, self.X1[i], self.p(i, "ln_2.weight"), self.mean2[i], self.rstd2[i], dX,
+                           self.g(i, "ln_2.weight"), self.g(i, "ln_2.bias"), dres=dX)
             # ---- attention: X1 = X + out_proj(attn(ln_1(X)))
             ops.gemm_nt(dX, self.wt(i, "attn.out_proj.weight"), self.dO, epilogue=ops.EPI_NONE)
             if trainable_w:
@@ -253,8 +252,8 @@ class _Tower:
             ops.gemm_nt(self.dQKV, self.wt(i, "attn.in_proj_weight"), self.dH, epilogue=ops.EPI_NONE)
             if trainable_w:
                 self._dw(self.dQKV, self.H1, self.g(i, "attn.in_proj_weight"), self.g(i, "attn.in_proj_bias"))
-            ops.layernorm_bwd(self.dH, self.X[i], self.p(i, "ln_1.weight"), self.mean1[i], self.rstd1[i], dX,
-                              self.g(i, "ln_1.weight"), self.g(i, "ln_1.bias"), self.ln_ws, dres=dX)
+            self.e.lnb.bwd(self.dH, self.X[i], self.p(i, "ln_1.weight"), self.mean1[i], self.rstd1[i], dX,
+                           self.g(i, "ln_1.weight"), self.g(i, "ln_1.bias"), dres=dX)
             if 1 <= i <= n_prompted:
                 ops.prompt_inject_bwd(dX, N, L, self.row0, N_CTX, D, prompt_grads[i - 1], accumulate=False,
                                       zero_rows=True)
@@ -295,6 +294,7 @@ class MapleEngine:
                           True, 1)
         self._build_io()
         self.side = torch.cuda.Stream(device=self.device)
+        self.lnb = ops.LNGradBatch(self.device)
         self.overlap_towers = True  # False: both towers on the current stream (isolated kernel timing)
         self.step_count = 0
         self.momentum_initialised = False
@@ -412,10 +412,23 @@ class MapleEngine:
         self.Xpre = e(B * self.Lv, dv)
         self.pre_mean, self.pre_rstd = e(B * self.Lv, dt_=F32), e(B * self.Lv, dt_=F32)
         self.shared_ctx = e(N_CTX, dv)
-        self.vis_deep = [e(N_CTX, dv, dt_=F32) for _ in range(J - 1)]
-        self.txt_deep = [e(N_CTX, dt, dt_=F32) for _ in range(J - 1)]
-        self.g_vis_deep = [e(N_CTX, dv, dt_=F32) for _ in range(J - 1)]
-        self.g_txt_deep = [e(N_CTX, dt, dt_=F32) for _ in range(J - 1)]
+        # deep prompts (trainers/maple.py:194-215): the tower that owns a prompt parameter reads (and
+        # writes the gradient of) the parameter tensor itself; the other tower gets its projection
+        self.vis_deep, self.txt_deep, self.g_vis_deep, self.g_txt_deep = [], [], [], []
+        pl = "prompt_learner."
+        for i in range(J - 1):
+            if i % 2 == 0:
+                name = pl + f"compound_prompts_text_parameters.{i // 2}"
+                self.txt_deep.append(self.P[name])
+                self.g_txt_deep.append(self.G[name])
+                self.vis_deep.append(e(N_CTX, dv, dt_=F32))
+                self.g_vis_deep.append(e(N_CTX, dv, dt_=F32))
+            else:
+                name = pl + f"visual_deep_prompts_parameters.{(i - 1) // 2}"
+                self.vis_deep.append(self.P[name])
+                self.g_vis_deep.append(self.G[name])
+                self.txt_deep.append(e(N_CTX, dt, dt_=F32))
+                self.g_txt_deep.append(e(N_CTX, dt, dt_=F32))
         self.g_shared_ctx = e(N_CTX, dv)
         self.vis_post = e(B, dv)
         self.post_mean, self.post_rstd = e(B, dt_=F32), e(B, dt_=F32)
@@ -433,9 +446,7 @@ class MapleEngine:
         self.dimg, self.dtxt = e(B, E), e(K, E)
         self.d_vis_post, self.d_txt_final = e(B, dv), e(K, dt)
         self.dXpre = e(B * self.Lv, dv)
-        self.ln_ws_text = e(ops.layernorm_ws_floats(K, dt), dt_=F32)  # text tower runs on the side stream
-        self.ln_ws_small = e(max(ops.layernorm_ws_floats(max(B, K), dv), ops.layernorm_ws_floats(B * self.Lv, dv)),
-                             dt_=F32)
+
 
     def load_batch(self, images: torch.Tensor, labels: Optional[torch.Tensor] = None):
         """Copy a batch into the static input buffers (H2D when given host tensors)."""
@@ -455,11 +466,9 @@ class MapleEngine:
             b = P[pl + f"compound_prompt_projections.{i}.bias"]
             if i % 2 == 0:
                 t = P[pl + f"compound_prompts_text_parameters.{i // 2}"]
-                self.txt_deep[i].copy_(t)
                 ops.small_linear_fwd(t, w, b, self.vis_deep[i])
             else:
                 v = P[pl + f"visual_deep_prompts_parameters.{(i - 1) // 2}"]
-                self.vis_deep[i].copy_(v)
                 ops.small_linear_fwd(v, w, b, self.txt_deep[i])
 
     def _prompt_learner_bwd(self):
@@ -471,11 +480,10 @@ class MapleEngine:
             db = G[pl + f"compound_prompt_projections.{i}.bias"]
             if i % 2 == 0:
                 name = pl + f"compound_prompts_text_parameters.{i // 2}"
-                G[name].copy_(self.g_txt_deep[i])          # direct use as the text prompt
+                # G[name] already holds the text tower's gradient of the direct use (g_txt_deep[i])
                 ops.small_linear_bwd(self.g_vis_deep[i], P[name], w, G[name], dw, db, accumulate_dx=True)
             else:
                 name = pl + f"visual_deep_prompts_parameters.{(i - 1) // 2}"
-                G[name].copy_(self.g_vis_deep[i])
                 ops.small_linear_bwd(self.g_txt_deep[i], P[name], w, G[name], dw, db, accumulate_dx=True)
         # ctx: text-path grad (already in G[ctx]) + fp16(d shared_ctx . W)
         ops.small_linear_bwd(self.g_shared_ctx, P[pl + "ctx"], P[pl + "proj_lang_to_vis.weight"], G[pl + "ctx"],
@@ -536,8 +544,8 @@ class MapleEngine:
         t = self.txt
         ops.gemm_nt(self.dtxt, P["text_encoder.text_projection"], self.d_txt_final, epilogue=ops.EPI_NONE)
         t.dX.zero_()
-        ops.layernorm_bwd(self.d_txt_final, t.X[-1], P["text_encoder.ln_final.weight"], self.fin_mean, self.fin_rstd,
-                          t.dX, G["text_encoder.ln_final.weight"], G["text_encoder.ln_final.bias"], self.ln_ws_text,
+        self.lnb.bwd(self.d_txt_final, t.X[-1], P["text_encoder.ln_final.weight"], self.fin_mean, self.fin_rstd,
+                     t.dX, G["text_encoder.ln_final.weight"], G["text_encoder.ln_final.bias"],
                           row_index=self.eot_rows)
         t.backward(self.J - 1, self.g_txt_deep)
         # d ctx (text path): sum over classes of the rows 1..n_ctx of d prompts (fp16 result)
@@ -549,12 +557,12 @@ class MapleEngine:
         v = self.vis
         ops.gemm_nt(self.dimg, P["image_encoder.proj"], self.d_vis_post, epilogue=ops.EPI_NONE)
         v.dX.zero_()
-        ops.layernorm_bwd(self.d_vis_post, v.X[-1], P["image_encoder.ln_post.weight"], self.post_mean,
+        self.lnb.bwd(self.d_vis_post, v.X[-1], P["image_encoder.ln_post.weight"], self.post_mean,
                           self.post_rstd, v.dX, G["image_encoder.ln_post.weight"], G["image_encoder.ln_post.bias"],
-                          self.ln_ws_small, row_index=self.cls_rows)
+                     row_index=self.cls_rows)
         v.backward(self.J - 1, self.g_vis_deep)
-        ops.layernorm_bwd(v.dX, self.Xpre, P["image_encoder.ln_pre.weight"], self.pre_mean, self.pre_rstd, self.dXpre,
-                          G["image_encoder.ln_pre.weight"], G["image_encoder.ln_pre.bias"], self.ln_ws_small)
+        self.lnb.bwd(v.dX, self.Xpre, P["image_encoder.ln_pre.weight"], self.pre_mean, self.pre_rstd, self.dXpre,
+                     G["image_encoder.ln_pre.weight"], G["image_encoder.ln_pre.bias"])
         ops.prompt_inject_bwd(self.dXpre, self.B, self.Lv, self.G2 + 1, N_CTX, v.D, self.g_shared_ctx,
                               accumulate=False, zero_rows=False)
 
@@ -571,6 +579,7 @@ class MapleEngine:
             self._text_backward()
         self._vision_backward()
         main.wait_stream(side)
+        self.lnb.finish()  # every LayerNorm's dgamma/dbeta in one reduction launch
         self._prompt_learner_bwd()
 
     # ------------------------------------------------------------------ optimizer

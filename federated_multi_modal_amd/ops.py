@@ -112,6 +112,50 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, workspace=None, d
     return dx
 
 
+class LNGradBatch:
+    """Deferred dgamma/dbeta reductions of every LayerNorm backward of a pass: each LN param pair gets
+    its own partial-sum workspace, and one mf_col_reduce_batch launch at the end of the backward
+    reduces them all (instead of one reduction launch per LayerNorm)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.ws = {}          # dgamma data_ptr -> workspace
+        self.descs = []       # (part_ptr, out_ptr, nblk, C)
+        self.keys = []
+        self.dev_descs = None
+        self.max_cols = 0
+
+    def bwd(self, dy, x, gamma, mean, rstd, dx, dgamma, dbeta, dres=None, row_index=None):
+        rows, D = dy.shape
+        key = dgamma.data_ptr()
+        if key not in self.ws:
+            nblk = call("mf_layernorm_bwd_blocks", rows)
+            w = torch.empty(2 * nblk * D, device=self.device, dtype=torch.float32)
+            self.ws[key] = w
+            self.descs.append((w.data_ptr(), dgamma.data_ptr(), nblk, D))
+            self.descs.append((w.data_ptr() + 4 * nblk * D, dbeta.data_ptr(), nblk, D))
+            self.max_cols = max(self.max_cols, D)
+            self.dev_descs = None
+        call("mf_layernorm_bwd", _p(dy), _ld(dy), _p(x), _ld(x), _p(row_index), _p(gamma), _p(mean), _p(rstd),
+             _p(dres), _ld(dres) if dres is not None else 0, _p(dx), _ld(dx), None, None, _p(self.ws[key]), rows, D,
+             0, _s())
+        return dx
+
+    def finish(self):
+        if not self.descs:
+            return
+        if self.dev_descs is None:
+            import numpy as np
+            assert call("mf_col_reduce_desc_bytes") == 32
+            arr = np.zeros(len(self.descs), dtype=np.dtype([("part", np.uint64), ("out", np.uint64),
+                                                            ("nblk", np.int32), ("C", np.int32),
+                                                            ("acc", np.int32), ("pad", np.int32)]))
+            for i, (pp, op, nb, c) in enumerate(self.descs):
+                arr[i] = (pp, op, nb, c, 0, 0)
+            self.dev_descs = torch.from_numpy(arr.view(np.uint8)).to(self.device)
+        call("mf_col_reduce_batch", _p(self.dev_descs), len(self.descs), self.max_cols, _s())
+
+
 def attention_fwd(qkv, N, L, H, causal, out=None, lse=None, ld_lse=None):
     D = H * 64
     if out is None:

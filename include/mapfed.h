@@ -52,6 +52,13 @@ int mf_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, c
                      void* dx, int64_t lddx, float* dgamma, float* dbeta, float* workspace, int rows, int D,
                      int accumulate, void* stream);
 
+/* dgamma == dbeta == NULL: write the per-block partials only; their reduction is deferred to one
+ * mf_col_reduce_batch over all LayerNorms of a backward pass.  desc = {const float* part; float* out;
+ * int nblk, C, accumulate, pad} (mf_col_reduce_desc_bytes() bytes each, device memory):
+ * out[c] (=|+=) sum_b part[b*C + c], fixed order.                                                  */
+int mf_col_reduce_desc_bytes(void);
+int mf_col_reduce_batch(const void* descs, int n, int max_cols, void* stream);
+
 /* ---- attention (head_dim 64, L <= 256; SDPA inside nn.MultiheadAttention, clip/model.py:303-305,
  * causal mask clip/model.py:679-685) — qkv [N*L, 3*H*64], out [N*L, H*64], lse [N*H, ld_lse]       */
 int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* lse, int ld_lse, int N,
