@@ -190,6 +190,145 @@ __global__ __launch_bounds__(512, 4) void attn_fwd_kernel(const f16* __restrict_
   }
 }
 
+// Forward, one workgroup per (sequence, head): K and V of the head are staged into LDS ONCE and
+// every wave owns QT 16-query tiles (32 queries at QT = 2), so each K / V^T fragment read from LDS
+// feeds QT MFMAs.  Same two-pass numerics as attn_fwd_kernel (P relative to the final row max).
+template <int LKP, bool CAUSAL, int QT>
+__global__ __launch_bounds__(64 * ((LKP + 16 * QT - 1) / (16 * QT)), 2) void attn_fwd2_kernel(
+    const f16* __restrict__ qkv, int64_t ld_qkv, f16* __restrict__ out, int64_t ld_out, float* __restrict__ lse,
+    int ld_lse, int L, int H) {
+  constexpr int NKT = LKP / 16;
+  __shared__ __attribute__((aligned(16))) f16 sK[LKP * 64];
+  __shared__ __attribute__((aligned(16))) f16 sV[LKP * 64];
+  const int D = H * 64;
+  const int nh = blockIdx.x, n = nh / H, h = nh % H;
+  const f16* base = qkv + (int64_t)n * L * ld_qkv;
+  stage_rows<LKP>(sK, base, ld_qkv, L, D + h * 64);
+  stage_rows<LKP>(sV, base, ld_qkv, L, 2 * D + h * 64);
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4, ii = lane & 15;
+  const int q0 = w * 16 * QT;
+  // Q fragments straight to registers (overlapping the K / V DMA)
+  f16x8 qf[QT][2];
+  int qrow[QT];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    qrow[t] = q0 + 16 * t + fr;
+    const int qc = qrow[t] < L ? qrow[t] : L - 1;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) qf[t][s] = *(const f16x8*)(base + (int64_t)qc * ld_qkv + h * 64 + 32 * s + 8 * fg);
+  }
+  int koff[2][2], voff[4][2];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int row = 16 * hf + fr;
+      koff[s2][hf] = row * 64 + (((4 * s2 + fg) ^ (row & 7)) << 3);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) voff[dt][hf] = sw_off(16 * hf + 4 * fg + (ii >> 2), 16 * dt + 4 * (ii & 3));
+  }
+  stage_wait();
+  const int kt_end = CAUSAL ? min(NKT, (q0 + 16 * QT + 15) / 16) : NKT;
+  const int ks_end = (kt_end + 1) / 2;
+  auto scores = [&](int ks, f32x4 (&a)[QT][2]) {
+    const f16* kb = sK + ks * 32 * 64;
+#pragma unroll
+    for (int t = 0; t < QT; ++t) a[t][0] = a[t][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const f16x8 k0 = *(const f16x8*)(kb + koff[s2][0]);
+      const f16x8 k1 = *(const f16x8*)(kb + koff[s2][1]);
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        a[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k0, qf[t][s2], a[t][0], 0, 0, 0);
+        a[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k1, qf[t][s2], a[t][1], 0, 0, 0);
+      }
+    }
+    if (CAUSAL || 32 * ks + 32 > L) {
+#pragma unroll
+      for (int t = 0; t < QT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key0 = 32 * ks + 4 * fg + i, key1 = key0 + 16;
+          if (key0 >= L || (CAUSAL && key0 > qrow[t])) a[t][0][i] = -INFINITY;
+          if (key1 >= L || (CAUSAL && key1 > qrow[t])) a[t][1][i] = -INFINITY;
+        }
+    }
+  };
+  float m[QT];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) m[t] = -INFINITY;
+#pragma unroll 1
+  for (int ks = 0; ks < ks_end; ++ks) {
+    f32x4 a[QT][2];
+    scores(ks, a);
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      m[t] = fmaxf(m[t], fmaxf(fmaxf(a[t][0][0], a[t][0][1]), fmaxf(a[t][0][2], a[t][0][3])));
+      m[t] = fmaxf(m[t], fmaxf(fmaxf(a[t][1][0], a[t][1][1]), fmaxf(a[t][1][2], a[t][1][3])));
+    }
+  }
+  constexpr float kLog2eScale = 0.125f * 1.4426950408889634f;
+  float mb[QT], l[QT];
+  f32x4 oacc[QT][4];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    m[t] = fmaxf(m[t], __shfl_xor(m[t], 16, 64));
+    m[t] = fmaxf(m[t], __shfl_xor(m[t], 32, 64));
+    mb[t] = -m[t] * kLog2eScale;
+    l[t] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) oacc[t][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll 1
+  for (int ks = 0; ks < ks_end; ++ks) {
+    f32x4 a[QT][2];
+    scores(ks, a);
+    f16x8 pf[QT];
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(a[t][0][i], kLog2eScale, mb[t]));
+        const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(a[t][1][i], kLog2eScale, mb[t]));
+        l[t] += p0 + p1;
+        pf[t][i] = (f16)p0;
+        pf[t][4 + i] = (f16)p1;
+      }
+    const f16* vb = sV + ks * 32 * 64;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[dt][0]));
+      s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[dt][1]));
+      const f16x8 vf = cat8(__builtin_bit_cast(f16x4, v0), __builtin_bit_cast(f16x4, v1));
+#pragma unroll
+      for (int t = 0; t < QT; ++t) oacc[t][dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[t], oacc[t][dt], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    float lt = l[t];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const int q = qrow[t];
+    if (q < L) {
+      const float inv = 1.0f / lt;
+      f16* orow = out + ((int64_t)n * L + q) * ld_out + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        f16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (f16)(oacc[t][dt][i] * inv);
+        *(f16x4*)(orow + 16 * dt + 4 * fg) = o;
+      }
+      if (fg == 0) lse[(int64_t)nh * ld_lse + q] = m[t] * kScale + __logf(lt);
+    }
+  }
+}
+
 // Dq[nh][q] = sum_d dO[q][d] * O[q][d] (fp32) ------------------------------------------------
 __global__ void attn_bwd_dot_kernel(const f16* __restrict__ out, int64_t ld_out, const f16* __restrict__ dout,
                                     int64_t ld_dout, float* __restrict__ dq_dot, int ld_lse, int N, int L, int H) {
@@ -409,8 +548,21 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
   if (L <= 0 || L > 256) return mf_set_error("mf_attention_fwd: 0 < L <= 256 required", -1);
   if (ld_lse < L || (ld_qkv % 8) || (ld_out % 4)) return mf_set_error("mf_attention_fwd: bad strides", -1);
   const int LP = padded_len(L);
-  const dim3 grid(N * H, attn_qsplit(N * H, L)), block(attn_threads(L));
   hipStream_t st = (hipStream_t)stream;
+  static const int fwd_variant = getenv("MAPFED_ATTN_FWD") ? atoi(getenv("MAPFED_ATTN_FWD")) : 2;  // A/B knob
+  if (fwd_variant == 2) {
+    const dim3 grid2(N * H), block2(64 * ((L + 31) / 32));
+#define CALLF2(P)                                                                                               \
+  if (causal)                                                                                                   \
+    attn_fwd2_kernel<P, true, 2><<<grid2, block2, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); \
+  else                                                                                                          \
+    attn_fwd2_kernel<P, false, 2><<<grid2, block2, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H);
+    MF_ATTN_DISPATCH(LP, CALLF2)
+#undef CALLF2
+    MF_CHECK_LAUNCH();
+    return 0;
+  }
+  const dim3 grid(N * H, attn_qsplit(N * H, L)), block(attn_threads(L));
 #define CALLF(P)                                                                                            \
   if (causal)                                                                                               \
     attn_fwd_kernel<P, true><<<grid, block, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); \

@@ -42,9 +42,22 @@ struct GemmArgs {
 };
 
 // Elementwise epilogue on 8 consecutive columns (fp16 staged value t = the GEMM result rounded at
-// the reference's first rounding point: fp16(acc + bias) or fp16(acc)).
+// the reference's first rounding point: fp16(acc + bias) or fp16(acc)).  The global operand an
+// epilogue reads (residual R or pre-activation F) is fetched by epi_prefetch BEFORE the LDS
+// staging pass so its latency overlaps the staging; epi8 finishes with it.
 template <int EPI>
-MF_DEV void epi8(const GemmArgs& g, int64_t m, int n, int cnt, const f16* t) {
+constexpr bool epi_reads_aux() { return EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU; }
+
+template <int EPI>
+MF_DEV f16x8 epi_prefetch(const GemmArgs& g, int64_t m, int n, int cnt) {
+  f16x8 v = {};
+  if constexpr (epi_reads_aux<EPI>())
+    if (cnt == 8 && g.vec8) v = *(const f16x8*)(g.aux_in + m * g.ld_aux + n);
+  return v;
+}
+
+template <int EPI>
+MF_DEV void epi8(const GemmArgs& g, int64_t m, int n, int cnt, const f16* t, f16x8 aux) {
   f16* crow = (f16*)g.C + m * g.ldc + n;
   if (cnt == 8 && g.vec8) {
     f16x8 tv = *(const f16x8*)t;
@@ -52,9 +65,8 @@ MF_DEV void epi8(const GemmArgs& g, int64_t m, int n, int cnt, const f16* t) {
     if constexpr (EPI == EPI_NONE || EPI == EPI_BIAS) {
       out = tv;
     } else if constexpr (EPI == EPI_BIAS_RESID || EPI == EPI_RESID) {
-      f16x8 rr = *(const f16x8*)(g.aux_in + m * g.ld_aux + n);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) out[e] = (f16)((float)rr[e] + (float)tv[e]);
+      for (int e = 0; e < 8; ++e) out[e] = (f16)((float)aux[e] + (float)tv[e]);
     } else if constexpr (EPI == EPI_BIAS_GELU) {
       *(f16x8*)(g.aux_out + m * g.ld_aux + n) = tv;
 #pragma unroll
@@ -63,9 +75,8 @@ MF_DEV void epi8(const GemmArgs& g, int64_t m, int n, int cnt, const f16* t) {
         out[e] = (f16)quick_gelu16((float)tv[e], &t2);
       }
     } else if constexpr (EPI == EPI_DGELU) {
-      f16x8 ff = *(const f16x8*)(g.aux_in + m * g.ld_aux + n);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) out[e] = (f16)quick_gelu16_bwd((float)tv[e], (float)ff[e]);
+      for (int e = 0; e < 8; ++e) out[e] = (f16)quick_gelu16_bwd((float)tv[e], (float)aux[e]);
     }
     *(f16x8*)crow = out;
     return;
@@ -90,15 +101,120 @@ MF_DEV void epi8(const GemmArgs& g, int64_t m, int n, int cnt, const f16* t) {
 
 constexpr int BK = 64;
 
+// In-kernel timeline stamps for diagnostics (tests/diagnostics/gemm_stamps.cpp builds this file
+// with MF_GEMM_STAMPS defined); compiled out of libmapfed.so.
+#ifdef MF_GEMM_STAMPS
+__device__ unsigned long long* g_stamps;
+#define MF_STAMP(slot)                                                                             \
+  do {                                                                                             \
+    if (threadIdx.x == 0) {                                                                        \
+      unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                    \
+      g_stamps[(size_t)blockIdx.x * 8 + (slot)] = t_;                                              \
+      if ((slot) == 0) {                                                                           \
+        unsigned xcc_ = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));                     \
+        unsigned hw_ = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));                      \
+        g_stamps[(size_t)blockIdx.x * 8 + 6] = xcc_;                                               \
+        g_stamps[(size_t)blockIdx.x * 8 + 7] = hw_;                                                \
+      }                                                                                            \
+    }                                                                                              \
+  } while (0)
+#else
+#define MF_STAMP(slot) \
+  do {                 \
+  } while (0)
+#endif
+
 MF_DEV int swz(int row, int chunk) { return chunk ^ (row & 7); }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// s_waitcnt vmcnt(n) lgkmcnt(0): LDS-DMA of all but the n youngest VMEM ops landed AND every ds_read
+// of this wave completed (a buffer's readers are done before the barrier that follows)
+template <int N>
+MF_DEV void wait_vm_lgkm0() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (0 << 8) | ((N >> 4) << 14));
+}
 
 // s_waitcnt vmcnt(n) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt[5:4]<<14)
 template <int N>
 MF_DEV void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt");
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// Epilogue shared by both kernel families: the first fp16 rounding point in registers
+// (fp16(acc + bias) / fp16(acc)) staged through LDS as a [BM][BN+8] fp16 tile, then the whole
+// workgroup streams rows out with 16-byte accesses (full cache lines) applying the rest of the
+// epilogue (residual, QuickGELU, QuickGELU').  acc[i][j] holds C[m0 + mbase + i*16 + fr]
+// [n0 + nbase + j*16 + 4*fg + e], e = 0..3.  The caller has barriered the operand ring.
+template <int BM, int BN, int NT, int TM, int TN, int EPI>
+MF_DEV void epilogue_store(const GemmArgs& g, f16* lds, const f32x4 (&acc)[TM][TN], int m0, int n0, int mbase,
+                           int nbase, int tid, int fr, int fg) {
+  if constexpr (EPI == EPI_F32) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + mbase + i * 16 + fr;
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + nbase + j * 16 + 4 * fg;
+        if (n < g.N) *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = acc[i][j];
+      }
+    }
+  } else {
+    constexpr int LDC = BN + 8;
+    constexpr int CPR = BN / 8;    // 16-byte chunks per tile row
+    constexpr int RPP = NT / CPR;  // rows per pass
+    constexpr int NPASS = (BM + RPP - 1) / RPP;
+    f16* sC = lds;
+    const int c8 = tid % CPR;
+    const int n = n0 + 8 * c8;
+    const int cnt = min(8, g.N - n);
+    const int r0 = tid / CPR;
+    // global operands first: residual / pre-activation rows of this thread's store passes, bias
+    f16x8 auxv[NPASS];
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const int m = m0 + r0 + p * RPP;
+      auxv[p] = (cnt > 0 && r0 + p * RPP < BM && m < g.M) ? epi_prefetch<EPI>(g, m, n, cnt) : f16x8{};
+    }
+    f16x4 bv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU)
+        bv[j] = *(const f16x4*)(g.bias + min(n0 + nbase + j * 16 + 4 * fg, g.N - 4));
+      else
+        bv[j] = f16x4{};
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml = mbase + i * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nl = nbase + j * 16 + 4 * fg;
+        f32x4 v = acc[i][j];
+        f16x4 t;
+        if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) t[e] = (f16)(v[e] + (float)bv[j][e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) t[e] = (f16)v[e];
+        }
+        *(f16x4*)(sC + ml * LDC + nl) = t;
+      }
+    }
+    __syncthreads();
+    if (cnt > 0) {
+#pragma unroll
+      for (int p = 0; p < NPASS; ++p) {
+        const int r = r0 + p * RPP;
+        const int m = m0 + r;
+        if (r < BM && m < g.M) epi8<EPI>(g, m, n, cnt, sC + r * LDC + 8 * c8, auxv[p]);
+      }
+    }
+  }
 }
 
 // Tile BM x BN, (WM x WN) waves each owning a (BM/WM) x (BN/WN) block of 16x16 MFMA tiles, BK = 64.
@@ -172,6 +288,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  MF_STAMP(0);
   const int nk = g.K / BK;
   // prologue: S-1 stages in flight
 #pragma unroll
@@ -191,6 +308,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g) {
       wait_vmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();
+    if (kt == 0) MF_STAMP(1);
     if (kt + S - 1 < nk) stage((kt + S - 1) % S, (kt + S - 1) * BK);
     const f16* la = lds + (kt % S) * STAGE;
     const f16* lb = la + BM * BK;
@@ -221,58 +339,215 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g) {
   }
 
   // epilogue.  lane holds C[m = .. + fr][n = .. + 4*fg + e], e = 0..3.
-  if constexpr (EPI == EPI_F32) {
+  MF_STAMP(2);
+  __syncthreads();  // every wave is done with the operand ring
+  epilogue_store<BM, BN, NT, TM, TN, EPI>(g, lds, acc, m0, n0, wave_m * WTM, wave_n * WTN, tid, fr, fg);
+  MF_STAMP(3);
+}
+
+// ------------------------------------------------------------------------------------------------
+// gemm8: 8 waves (512 threads), BM x BN tile with BM = 256, one workgroup per CU (two LDS buffers of
+// (BM+BN) x 64 fp16), phase-interleaved pipeline after cdna_hip_programming.md §5 "256^2 8-phase
+// template" / T3+T4, restated for this kernel:
+//   * each wave owns a WTM x WTN block of C, split into 2 x 2 quadrants (QM x QN);  a K-tile
+//     (BK = 64) is computed in 4 phases, one quadrant each, in the order (0,0) (0,1) (1,1) (1,0):
+//     A fragments of m-half 0 serve phases 0-1, B fragments of n-half 1 serve phases 1-2, the
+//     n-half-0 B fragments stay in registers from phase 0 to phase 3;
+//   * the LDS image of a K-tile is four "half-tiles" (A rows of m-half 0 / 1 across both wave rows,
+//     B rows of n-half 0 / 1 across the four wave columns); the glds loads of K-tile t+1 are issued
+//     one half-tile per phase of K-tile t (A0, B0, B1, A1), so two half-tiles are always in flight
+//     across the barriers: each phase waits only for the half-tile it is about to read (counted
+//     s_waitcnt vmcnt, never 0 in the loop) and one raw s_barrier makes every wave's DMA visible;
+//   * WAR: a half-tile of buffer b is overwritten only in the K-tile after the one that read it,
+//     i.e. behind at least one barrier every wave passed after its last ds_read of it.
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
+  constexpr int NW = 8, NT = 512;
+  static_assert(WM * WN == NW, "8 waves");
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int QM = WTM / 2, QN = WTN / 2;
+  constexpr int QTM = QM / 16, QTN = QN / 16;
+  static_assert(QTM >= 1 && QTN >= 1 && QM % 8 == 0 && QN % 8 == 0, "quadrant shape");
+  constexpr int A_INS = BM / 128;  // glds wave-instructions per wave per A half-tile (BM/2 rows / 8 / 8 waves)
+  constexpr int B_INS = BN / 128;
+  static_assert(A_INS >= 1 && B_INS >= 1 && A_INS * 128 == BM && B_INS * 128 == BN, "half-tile split");
+  constexpr int BUF = (BM + BN) * BK;  // fp16 elements per K-tile buffer
+  constexpr int LDC = BN + 8;
+  constexpr int LDS_ELEMS = 2 * BUF > BM * LDC ? 2 * BUF : BM * LDC;
+  __shared__ __attribute__((aligned(1024))) f16 lds[LDS_ELEMS];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int m0 = (wgid / tiles_n) * BM;
+  const int n0 = (wgid % tiles_n) * BN;
+
+  // LDS-DMA sources / destinations.  Half-tile h of A = tile rows {s*WTM + h*QM + [0, QM)} for
+  // s < WM, i.e. BM/16 blocks of 8 rows; wave w loads blocks w*A_INS + i.  Same for B with
+  // (WN, WTN, QN).  Loads are buffer_load ... lds through a buffer descriptor sized to the operand:
+  // rows past M (N) read as zero (no clamping, no per-lane pointers); the per-lane byte offset is
+  // shared by every load of an operand and the row/K position goes in the scalar offset.
+  const int lrow = lane >> 3;
+  const int lchunk = (lane & 7) ^ lrow;  // source pre-swizzled: LDS chunk c of row r holds chunk c ^ (r & 7)
+  const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.A, 0, (int)(((int64_t)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t b_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.B, 0, (int)(((int64_t)(g.N - 1) * g.ldb + g.K) * 2), 0x00020000);
+  const int a_voff = (lrow * (int)g.lda + lchunk * 8) * 2;
+  const int b_voff = (lrow * (int)g.ldb + lchunk * 8) * 2;
+  auto a_row = [&](int h, int i) {  // first tile row of this wave's i-th block of A half-tile h
+    const int blk = wid * A_INS + i;
+    return (blk / (QM / 8)) * WTM + h * QM + (blk % (QM / 8)) * 8;
+  };
+  auto b_row = [&](int h, int i) {
+    const int blk = wid * B_INS + i;
+    return (blk / (QN / 8)) * WTN + h * QN + (blk % (QN / 8)) * 8;
+  };
+  auto load_a = [&](int buf, int h, int k0) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wave_m * WTM + i * 16 + fr;
-      if (m >= g.M) continue;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wave_n * WTN + j * 16 + 4 * fg;
-        if (n < g.N) *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = acc[i][j];
-      }
+    for (int i = 0; i < A_INS; ++i) {
+      const int row = a_row(h, i);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(lds + buf * BUF + row * BK), 16, a_voff,
+                                               (int)(((int64_t)(m0 + row) * g.lda + k0) * 2), 0, 0);
     }
-  } else {
-    // 1) the first fp16 rounding point in registers (fp16(acc + bias) / fp16(acc)), staged through LDS
-    //    as a [BM][BN+8] fp16 tile; 2) the whole workgroup streams rows out with 16-byte accesses
-    //    (full cache lines) applying the rest of the epilogue (residual, QuickGELU, QuickGELU').
-    constexpr int LDC = BN + 8;
-    f16* sC = lds;
-    __syncthreads();  // every wave is done with the operand ring
+  };
+  auto load_b = [&](int buf, int h, int k0) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int ml = wave_m * WTM + i * 16 + fr;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int nl = wave_n * WTN + j * 16 + 4 * fg;
-        f32x4 v = acc[i][j];
-        f16x4 t;
-        if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU) {
-          const int n = min(n0 + nl, g.N - 4);
-          f16x4 b = *(const f16x4*)(g.bias + n);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) t[e] = (f16)(v[e] + (float)b[e]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) t[e] = (f16)v[e];
-        }
-        *(f16x4*)(sC + ml * LDC + nl) = t;
-      }
+    for (int i = 0; i < B_INS; ++i) {
+      const int row = b_row(h, i);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_ptr_t)(lds + buf * BUF + BM * BK + row * BK), 16, b_voff,
+                                               (int)(((int64_t)(n0 + row) * g.ldb + k0) * 2), 0, 0);
     }
-    __syncthreads();
-    constexpr int CPR = BN / 8;        // 16-byte chunks per tile row
-    constexpr int RPP = NT / CPR;      // rows per pass
-    const int c8 = tid % CPR;
-    const int n = n0 + 8 * c8;
-    const int cnt = min(8, g.N - n);
-    if (cnt > 0) {
-#pragma unroll 4
-      for (int r = tid / CPR; r < BM; r += RPP) {
-        const int m = m0 + r;
-        if (m < g.M) epi8<EPI>(g, m, n, cnt, sC + r * LDC + 8 * c8);
+  };
+
+  constexpr int TM = 2 * QTM, TN = 2 * QTN;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fg = lane >> 4;
+  auto read_a = [&](f16x8 (&af)[2][QTM], const f16* base, int mh) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < QTM; ++i) {
+        const int row = wm * WTM + mh * QM + i * 16 + fr;
+        af[s][i] = *(const f16x8*)(base + row * BK + swz(row, 4 * s + fg) * 8);
       }
+  };
+  auto read_b = [&](f16x8 (&bf)[2][QTN], const f16* base, int nh) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < QTN; ++j) {
+        const int row = wn * WTN + nh * QN + j * 16 + fr;
+        bf[s][j] = *(const f16x8*)(base + BM * BK + row * BK + swz(row, 4 * s + fg) * 8);
+      }
+  };
+  auto mma = [&](const f16x8 (&af)[2][QTM], const f16x8 (&bf)[2][QTN], int mh, int nh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < QTM; ++i)
+#pragma unroll
+        for (int j = 0; j < QTN; ++j)
+          acc[mh * QTM + i][nh * QTN + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[s][j], af[s][i], acc[mh * QTM + i][nh * QTN + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  MF_STAMP(0);
+  const int nk = g.K / BK;
+  // prologue: the four half-tiles of K-tile 0 in the order the loop consumes them; retire A0, B0,
+  // B1 and read the fragments of phase 0 (A0, B0)
+  load_a(0, 0, 0);
+  load_b(0, 0, 0);
+  load_b(0, 1, 0);
+  load_a(0, 1, 0);
+  f16x8 fa0[2][QTM], fa1[2][QTM], fb0[2][QTN], fb1[2][QTN];
+  wait_vm_lgkm0<A_INS>();
+  __builtin_amdgcn_s_barrier();
+  read_a(fa0, lds, 0);
+  read_b(fb0, lds, 0);
+
+  // Phase p of K-tile kt: ds_reads of phase p+1's fragments (their half-tile was retired by the
+  // barrier that opened phase p), one half-tile of glds for K-tile kt+1 (issue order A0 B0 B1 A1),
+  // the MFMAs of phase p on fragments read during phase p-1; then, where phase p+2 reads a new
+  // half-tile, a counted vmcnt + lgkmcnt(0) and a barrier.  Every ds_read of a buffer completes
+  // before the barrier that ends its phase, and a buffer is refilled only in the K-tile after the
+  // one that read it, so all WAR distances are >= 1 barrier.
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cb = kt & 1;
+    const f16* base = lds + cb * BUF;
+    const f16* nbase = lds + (cb ^ 1) * BUF;
+    const bool more = kt + 1 < nk;
+    const int k1 = (kt + 1) * BK;
+    // phase 0: quadrant (0,0); reads B1(kt); retire A1(kt) for phase 1's reads (younger: A0(kt+1))
+    read_b(fb1, base, 1);
+    if (more) load_a(cb ^ 1, 0, k1);
+    mma(fa0, fb0, 0, 0);
+    if (more) wait_vm_lgkm0<A_INS>();
+    else wait_vm_lgkm0<0>();
+    __builtin_amdgcn_s_barrier();
+    // phase 1: quadrant (0,1); reads A1(kt)
+    read_a(fa1, base, 1);
+    if (more) load_b(cb ^ 1, 0, k1);
+    mma(fa0, fb1, 0, 1);
+    // phase 2: quadrant (1,1); re-reads B0(kt); retire A0(kt+1), B0(kt+1) (younger: B1(kt+1))
+    read_b(fb0, base, 0);
+    if (more) {
+      load_b(cb ^ 1, 1, k1);
+      mma(fa1, fb1, 1, 1);
+      wait_vm_lgkm0<B_INS>();
+      __builtin_amdgcn_s_barrier();
+      // phase 3: quadrant (1,0); reads A0(kt+1), B0(kt+1); retire B1(kt+1) (younger: A1(kt+1))
+      f16x8 nb0[2][QTN];
+      read_a(fa0, nbase, 0);
+      read_b(nb0, nbase, 0);
+      load_a(cb ^ 1, 1, k1);
+      mma(fa1, fb0, 1, 0);
+      wait_vm_lgkm0<A_INS>();
+      __builtin_amdgcn_s_barrier();
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < QTN; ++j) fb0[s2][j] = nb0[s2][j];
+    } else {
+      mma(fa1, fb1, 1, 1);
+      mma(fa1, fb0, 1, 0);
     }
   }
+
+  __syncthreads();  // every wave is done with the operand ring (no DMA outstanding after the last K-tile)
+  epilogue_store<BM, BN, NT, TM, TN, EPI>(g, lds, acc, m0, n0, wm * WTM, wn * WTN, tid, fr, fg);
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_tile8(const GemmArgs& a, int epi, hipStream_t st) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles), block(512);
+  switch (epi) {
+    case EPI_NONE: gemm8_kernel<BM, BN, WM, WN, EPI_NONE><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS: gemm8_kernel<BM, BN, WM, WN, EPI_BIAS><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_RESID: gemm8_kernel<BM, BN, WM, WN, EPI_BIAS_RESID><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_GELU: gemm8_kernel<BM, BN, WM, WN, EPI_BIAS_GELU><<<grid, block, 0, st>>>(a); break;
+    case EPI_DGELU: gemm8_kernel<BM, BN, WM, WN, EPI_DGELU><<<grid, block, 0, st>>>(a); break;
+    case EPI_F32: gemm8_kernel<BM, BN, WM, WN, EPI_F32><<<grid, block, 0, st>>>(a); break;
+    case EPI_RESID: gemm8_kernel<BM, BN, WM, WN, EPI_RESID><<<grid, block, 0, st>>>(a); break;
+    default: return mf_set_error("mf_gemm_nt: bad epilogue", -2);
+  }
+  MF_CHECK_LAUNCH();
+  return 0;
 }
 
 template <int BM, int BN, int WM, int WN, int S>
@@ -330,6 +605,11 @@ extern "C" int mf_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb
     case 12: return launch_tile<256, 128, 2, 2, 2>(a, epilogue, st);
     case 13: return launch_tile<128, 256, 2, 2, 3>(a, epilogue, st);
     case 14: return launch_tile<128, 64, 2, 2, 4>(a, epilogue, st);
+    case 20: return launch_tile8<256, 256, 2, 4>(a, epilogue, st);
+    case 21: return launch_tile8<256, 128, 2, 4>(a, epilogue, st);
+    case 22: return launch_tile8<256, 128, 4, 2>(a, epilogue, st);
+    case 23: return launch_tile8<128, 256, 2, 4>(a, epilogue, st);
+    case 24: return launch_tile8<128, 128, 2, 4>(a, epilogue, st);
     default: return mf_set_error("mf_gemm_nt: bad tile id", -2);
   }
 }

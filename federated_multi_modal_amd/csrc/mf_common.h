@@ -32,9 +32,13 @@ MF_DEV float wave_max(float v) {
 
 // QuickGELU with the reference's three fp16 roundings (clip/model.py:162-164):
 //   t1 = fp16(1.702*f); t2 = fp16(sigmoid(t1)); g = fp16(f*t2)
+// sigmoid in fp32 with the hardware reciprocal (v_rcp_f32, 1 ulp): its result is rounded to fp16
+// next, so the fp32 ulp matters only within 2^-13 of an fp16 rounding boundary
+MF_DEV float sigmoid32(float t) { return __builtin_amdgcn_rcpf(1.0f + __expf(-t)); }
+
 MF_DEV float quick_gelu16(float f, float* t2_out) {
   float t1 = r16(f * 1.702f);
-  float t2 = r16(1.0f / (1.0f + __expf(-t1)));
+  float t2 = r16(sigmoid32(t1));
   *t2_out = t2;
   return r16(f * t2);
 }
@@ -44,7 +48,7 @@ MF_DEV float quick_gelu16(float f, float* t2_out) {
 //   aten::sigmoid_backward): dt1 = fp16(fp16(dt2*fp16(1-t2))*t2)
 MF_DEV float quick_gelu16_bwd(float dg, float f) {
   float t1 = r16(f * 1.702f);
-  float t2 = r16(1.0f / (1.0f + __expf(-t1)));
+  float t2 = r16(sigmoid32(t1));
   float da = r16(dg * t2);
   float dt2 = r16(dg * f);
   float dt1 = r16(r16(dt2 * r16(1.0f - t2)) * t2);

@@ -1,5 +1,9 @@
-"""Diagnostic (GPU box): time every mf_gemm_nt tile configuration on the MaPLe step's GEMM shapes,
-check each against a torch fp32 matmul, print TFLOP/s.  Usage: python gemm_bench.py [tiles]"""
+"""Diagnostic (GPU box): time mf_gemm_nt on the MaPLe step's GEMM shapes (c4: vision M = 32*199,
+text M = 38*77), against hipBLASLt (torch.mm, plain product, no epilogue) as a yardstick, and check
+each tile configuration against a torch fp32 matmul.  Prints TFLOP/s.
+
+    python gemm_bench.py [tiles]        tiles: comma list of mf_gemm_nt tile ids (0 = heuristic)
+"""
 import sys
 from pathlib import Path
 
@@ -8,23 +12,39 @@ import torch
 sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 from federated_multi_modal_amd import ops  # noqa: E402
 
-SHAPES = [  # (name, M, N, K, epilogue)
-    ("v.qkv", 6368, 2304, 768, ops.EPI_BIAS), ("v.out", 6368, 768, 768, ops.EPI_BIAS_RESID),
-    ("v.fc", 6368, 3072, 768, ops.EPI_BIAS_GELU), ("v.proj", 6368, 768, 3072, ops.EPI_BIAS_RESID),
-    ("v.dfc", 6368, 3072, 768, ops.EPI_DGELU), ("v.dh", 6368, 768, 3072, ops.EPI_NONE),
-    ("v.dqkv", 6368, 768, 2304, ops.EPI_NONE),
-    ("t.qkv", 2926, 1536, 512, ops.EPI_BIAS), ("t.fc", 2926, 2048, 512, ops.EPI_BIAS_GELU),
-    ("t.proj", 2926, 512, 2048, ops.EPI_BIAS_RESID), ("t.dh", 2926, 512, 2048, ops.EPI_NONE),
-    ("v.dW_fc", 3072, 768, 6400, ops.EPI_NONE),
+SHAPES = [  # (name, M, N, K, epilogue, calls per c4 step)
+    ("v.qkv", 6368, 2304, 768, ops.EPI_BIAS, 12), ("v.out", 6368, 768, 768, ops.EPI_BIAS_RESID, 12),
+    ("v.fc", 6368, 3072, 768, ops.EPI_BIAS_GELU, 12), ("v.proj", 6368, 768, 3072, ops.EPI_BIAS_RESID, 12),
+    ("v.dfc", 6368, 3072, 768, ops.EPI_DGELU, 12), ("v.dh", 6368, 768, 3072, ops.EPI_NONE, 12),
+    ("v.do", 6368, 768, 768, ops.EPI_NONE, 12), ("v.dqkv", 6368, 768, 2304, ops.EPI_NONE, 12),
+    ("t.qkv", 2926, 1536, 512, ops.EPI_BIAS, 12), ("t.out", 2926, 512, 512, ops.EPI_BIAS_RESID, 12),
+    ("t.fc", 2926, 2048, 512, ops.EPI_BIAS_GELU, 12), ("t.proj", 2926, 512, 2048, ops.EPI_BIAS_RESID, 12),
+    ("t.dfc", 2926, 2048, 512, ops.EPI_DGELU, 12), ("t.dh", 2926, 512, 2048, ops.EPI_NONE, 12),
+    ("t.do", 2926, 512, 512, ops.EPI_NONE, 12), ("t.dqkv", 2926, 512, 1536, ops.EPI_NONE, 12),
+    ("v.dW_fc", 3072, 768, 6400, ops.EPI_NONE, 1), ("v.dW_qkv", 2304, 768, 6400, ops.EPI_NONE, 1),
 ]
 
 
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3  # us
+
+
 def main():
-    tiles = [int(t) for t in sys.argv[1].split(",")] if len(sys.argv) > 1 else list(range(1, 10))
+    tiles = [int(t) for t in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0]
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    print(f"{'shape':10s} " + " ".join(f"{'t' + str(t):>8s}" for t in tiles), flush=True)
-    for name, M, N, K, epi in SHAPES:
+    print(f"{'shape':10s} {'blasLt':>8s} " + " ".join(f"{'t' + str(t):>8s}" for t in tiles) + "   (TFLOP/s; "
+          "last col: us/step at heuristic tile)", flush=True)
+    tot_us, tot_blas = 0.0, 0.0
+    for name, M, N, K, epi, calls in SHAPES:
         A = torch.randn(M, K, device=dev).half()
         B = (torch.randn(N, K, device=dev) * K ** -0.5).half()
         bias = torch.randn(N, device=dev).half() * 0.1
@@ -32,6 +52,9 @@ def main():
         auxo = torch.empty(M, N, device=dev, dtype=torch.float16)
         C = torch.empty(M, N, device=dev, dtype=torch.float16)
         ref = (A.float() @ B.float().t())
+        fl = 2 * M * N * K
+        ub = timeit(lambda: torch.mm(A, B.t(), out=C))
+        tot_blas += ub * calls
         res = []
         for t in tiles:
             kw = dict(C=C, epilogue=epi, tile=t)
@@ -43,26 +66,18 @@ def main():
                 kw["aux_out"] = auxo
             try:
                 ops.gemm_nt(A, B, **kw)
-            except Exception as e:  # noqa: BLE001
+                C0 = ops.gemm_nt(A, B, epilogue=ops.EPI_NONE, tile=t)
+            except Exception:  # noqa: BLE001
                 res.append("   err")
                 continue
-            # correctness of the raw product through EPI_NONE
-            C0 = ops.gemm_nt(A, B, epilogue=ops.EPI_NONE, tile=t)
             err = (C0.float() - ref).abs().max().item()
             ok = err < 2e-2 * ref.abs().max().item()
-            torch.cuda.synchronize()
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            for _ in range(3):
-                ops.gemm_nt(A, B, **kw)
-            s.record()
-            for _ in range(20):
-                ops.gemm_nt(A, B, **kw)
-            e.record()
-            torch.cuda.synchronize()
-            us = s.elapsed_time(e) / 20 * 1e3
-            tf = 2 * M * N * K / us / 1e6
-            res.append(f"{tf:7.0f}{'' if ok else '!'}")
-        print(f"{name:10s} " + " ".join(f"{r:>8s}" for r in res), flush=True)
+            us = timeit(lambda: ops.gemm_nt(A, B, **kw))
+            if t == tiles[0]:
+                tot_us += us * calls
+            res.append(f"{fl / us / 1e6:7.0f}{'' if ok else '!'}")
+        print(f"{name:10s} {fl / ub / 1e6:8.0f} " + " ".join(f"{r:>8s}" for r in res), flush=True)
+    print(f"sum over a c4 step: ours (tile {tiles[0]}) {tot_us / 1e3:.2f} ms, hipBLASLt plain {tot_blas / 1e3:.2f} ms")
 
 
 if __name__ == "__main__":

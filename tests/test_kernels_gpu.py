@@ -30,7 +30,12 @@ def assert_ulps(out, ref, max_ulp=1.0, frac=1e-2, what="", floor=2e-5):
 
 
 @pytest.mark.parametrize("M,N,K,tile", [(796, 2304, 768, 0), (6368, 768, 3072, 0), (770, 512, 2048, 1),
-                                        (130, 44, 64, 3), (257, 1536, 512, 2), (6368, 3072, 768, 0)])
+                                        (130, 44, 64, 3), (257, 1536, 512, 2), (6368, 3072, 768, 0),
+                                        # 8-wave phase-pipelined family (tiles 20-24), ragged M / N
+                                        (6368, 2304, 768, 20), (1000, 760, 192, 20), (6368, 3072, 768, 21),
+                                        (300, 388, 64, 21), (6368, 768, 3072, 22), (777, 132, 128, 22),
+                                        (2926, 1536, 512, 23), (129, 260, 320, 23), (2926, 512, 2048, 24),
+                                        (65, 36, 64, 24)])
 def test_gemm_bias(dev, M, N, K, tile):
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g).half().to(dev)
@@ -52,7 +57,8 @@ def _gelu16(f):
     return (f.float() * t2.float()).half()
 
 
-def test_gemm_epilogues(dev):
+@pytest.mark.parametrize("tile", [0, 20, 22])
+def test_gemm_epilogues(dev, tile):
     torch.manual_seed(0)
     M, N, K = 600, 1024, 256
     A = torch.randn(M, K).half().to(dev)
@@ -62,23 +68,23 @@ def test_gemm_epilogues(dev):
     acc = A.double() @ B.double().t()
     y16 = (acc + b.double()).half()
     # residual
-    C = ops.gemm_nt(A, B, bias=b, aux_in=R, epilogue=ops.EPI_BIAS_RESID)
+    C = ops.gemm_nt(A, B, bias=b, aux_in=R, epilogue=ops.EPI_BIAS_RESID, tile=tile)
     ref = (R.float() + y16.float()).half()
     assert (C.float() - ref.float()).abs().max().item() <= 2 * ulp16(ref).max().item()
     assert (C != ref).float().mean().item() < 2e-2
     # residual in place (C aliases R)
     R2 = R.clone()
-    ops.gemm_nt(A, B, C=R2, bias=b, aux_in=R2, epilogue=ops.EPI_BIAS_RESID)
+    ops.gemm_nt(A, B, C=R2, bias=b, aux_in=R2, epilogue=ops.EPI_BIAS_RESID, tile=tile)
     assert torch.equal(R2, C)
     # gelu: stores pre-activation and QuickGELU with the reference's roundings
     Fpre = torch.empty(M, N, dtype=torch.float16, device=dev)
-    G = ops.gemm_nt(A, B, bias=b, aux_out=Fpre, epilogue=ops.EPI_BIAS_GELU)
+    G = ops.gemm_nt(A, B, bias=b, aux_out=Fpre, epilogue=ops.EPI_BIAS_GELU, tile=tile)
     assert (Fpre != y16).float().mean().item() < 2e-2
     assert (G != _gelu16(Fpre)).float().mean().item() < 1e-3
     # dgelu: the reference's autograd of QuickGELU on CPU torch (sigmoid_backward for Half runs in
     # fp16 op by op there), restated with explicit ops on the kernel's own fp16 GEMM output
-    dG = ops.gemm_nt(A, B, aux_in=Fpre, epilogue=ops.EPI_DGELU)
-    dg = ops.gemm_nt(A, B, epilogue=ops.EPI_NONE).float()
+    dG = ops.gemm_nt(A, B, aux_in=Fpre, epilogue=ops.EPI_DGELU, tile=tile)
+    dg = ops.gemm_nt(A, B, epilogue=ops.EPI_NONE, tile=tile).float()
     h = lambda t: t.half().float()
     ff = Fpre.float()
     t2 = h(torch.sigmoid(h(ff * 1.702)))
