@@ -549,7 +549,7 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
   if (ld_lse < L || (ld_qkv % 8) || (ld_out % 4)) return mf_set_error("mf_attention_fwd: bad strides", -1);
   const int LP = padded_len(L);
   hipStream_t st = (hipStream_t)stream;
-  static const int fwd_variant = getenv("MAPFED_ATTN_FWD") ? atoi(getenv("MAPFED_ATTN_FWD")) : 2;  // A/B knob
+  static const int fwd_variant = getenv("MAPFED_ATTN_FWD") ? atoi(getenv("MAPFED_ATTN_FWD")) : 1;  // A/B knob
   if (fwd_variant == 2) {
     const dim3 grid2(N * H), block2(64 * ((L + 31) / 32));
 #define CALLF2(P)                                                                                               \

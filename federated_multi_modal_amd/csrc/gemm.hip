@@ -15,6 +15,8 @@
 // one barrier per K-step; XCD-aware bijective block remap so tiles sharing an A panel share
 // an L2.  The MFMA is issued "swapped" (weight fragment as the A operand) so each lane ends with
 // 4 consecutive output columns of one row -> 8-byte stores.
+#include <type_traits>
+
 #include "mf_common.h"
 
 namespace {
@@ -127,6 +129,15 @@ __device__ unsigned long long* g_stamps;
 MF_DEV int swz(int row, int chunk) { return chunk ^ (row & 7); }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// Raw s_barrier that also stops the compiler from moving LDS accesses across it (the builtin alone
+// carries no memory semantics); unlike __syncthreads() it emits no vmcnt(0), so LDS-DMA stays in
+// flight across it.
+MF_DEV void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 // s_waitcnt vmcnt(n) lgkmcnt(0): LDS-DMA of all but the n youngest VMEM ops landed AND every ds_read
 // of this wave completed (a buffer's readers are done before the barrier that follows)
@@ -346,34 +357,40 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// gemm8: 8 waves (512 threads), BM x BN tile with BM = 256, one workgroup per CU (two LDS buffers of
-// (BM+BN) x 64 fp16), phase-interleaved pipeline after cdna_hip_programming.md §5 "256^2 8-phase
-// template" / T3+T4, restated for this kernel:
-//   * each wave owns a WTM x WTN block of C, split into 2 x 2 quadrants (QM x QN);  a K-tile
-//     (BK = 64) is computed in 4 phases, one quadrant each, in the order (0,0) (0,1) (1,1) (1,0):
-//     A fragments of m-half 0 serve phases 0-1, B fragments of n-half 1 serve phases 1-2, the
-//     n-half-0 B fragments stay in registers from phase 0 to phase 3;
-//   * the LDS image of a K-tile is four "half-tiles" (A rows of m-half 0 / 1 across both wave rows,
-//     B rows of n-half 0 / 1 across the four wave columns); the glds loads of K-tile t+1 are issued
-//     one half-tile per phase of K-tile t (A0, B0, B1, A1), so two half-tiles are always in flight
-//     across the barriers: each phase waits only for the half-tile it is about to read (counted
-//     s_waitcnt vmcnt, never 0 in the loop) and one raw s_barrier makes every wave's DMA visible;
-//   * WAR: a half-tile of buffer b is overwritten only in the K-tile after the one that read it,
-//     i.e. behind at least one barrier every wave passed after its last ds_read of it.
+// gemm8: 8 waves (512 threads), BM x BN tile with BM = 256 (or 128), one workgroup per CU.
+// Why this shape: a CU pulls operands from L2 at roughly 64-70 GB/s (MI355X_MICROARCH.md, LDS gather
+// rates), so the tile's FLOP per fetched byte sets the MFMA ceiling: 128x128 needs ~150 GB/s per CU
+// at full MFMA rate (measured main loop 45-50 % of peak), 256x256 needs ~75 GB/s.
+// Pipeline (cdna_hip_programming.md §5 T3+T4, restated for this kernel): a K-tile (BK = 64) is four
+// phases (m-half, k-sub) in the order (0,0) (1,0) (1,1) (0,1); a phase issues the ds_reads of the
+// NEXT phase's fragments (from data retired by an earlier barrier) ahead of its own MFMAs, so LDS
+// latency hides under the matrix pipe.  The operands of a K-tile are four half-tiles
+// [A k0, B k0, A k1, B k1] (sequence number 4*kt + h), each a [rows][32] fp16 image (64-byte rows,
+// 16-byte chunk c of row r stored at c ^ ((-(r >> 2)) & 3): conflict-free ds_read_b128 fragment
+// reads, checked with the bank model).  They live in a ring of NSLOT = 10 slots of SLOT bytes
+// (160 KiB) and are filled by LDS-DMA (buffer_load ... lds, 16 rows x 64 B per wave instruction,
+// swizzle applied to the source) TWO K-tiles ahead, one half-tile per phase: ~8 phases of latency
+// cover before a counted vmcnt + barrier retires a pair (two such points per K-tile).  WAR: the
+// half-tile a load overwrites (sequence - 10) was last read at least one barrier earlier and every
+// ds_read completes (lgkmcnt(0)) before the next barrier.  A/B fragment register sets alternate
+// statically (no copies, no scratch); the loop is peeled so the steady-state body has no branches.
 template <int BM, int BN, int WM, int WN, int EPI>
 __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
-  constexpr int NW = 8, NT = 512;
-  static_assert(WM * WN == NW, "8 waves");
+  constexpr int NT = 512;
+  static_assert(WM * WN == 8, "8 waves");
   constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int QM = WTM / 2, QN = WTN / 2;
-  constexpr int QTM = QM / 16, QTN = QN / 16;
-  static_assert(QTM >= 1 && QTN >= 1 && QM % 8 == 0 && QN % 8 == 0, "quadrant shape");
-  constexpr int A_INS = BM / 128;  // glds wave-instructions per wave per A half-tile (BM/2 rows / 8 / 8 waves)
+  constexpr int QM = WTM / 2;
+  constexpr int QTM = QM / 16, TN = WTN / 16, TM = 2 * QTM;
+  static_assert(QTM >= 1 && TN >= 1 && QM % 16 == 0, "phase shape");
+  constexpr int A_INS = BM / 128;  // LDS-DMA wave instructions per wave per half-tile (rows x 64 B)
   constexpr int B_INS = BN / 128;
-  static_assert(A_INS >= 1 && B_INS >= 1 && A_INS * 128 == BM && B_INS * 128 == BN, "half-tile split");
-  constexpr int BUF = (BM + BN) * BK;  // fp16 elements per K-tile buffer
+  static_assert(A_INS * 128 == BM && B_INS * 128 == BN, "half-tile split");
+  constexpr int HK = 32;                                // k-sub width (elements)
+  constexpr int SLOT = (BM > BN ? BM : BN) * HK;        // fp16 elements per ring slot
+  constexpr int NSLOT = 10;
   constexpr int LDC = BN + 8;
-  constexpr int LDS_ELEMS = 2 * BUF > BM * LDC ? 2 * BUF : BM * LDC;
+  constexpr int LDS_ELEMS = NSLOT * SLOT > BM * LDC ? NSLOT * SLOT : BM * LDC;
+  static_assert(LDS_ELEMS * 2 <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(1024))) f16 lds[LDS_ELEMS];
 
   const int tid = threadIdx.x;
@@ -389,45 +406,37 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   const int m0 = (wgid / tiles_n) * BM;
   const int n0 = (wgid % tiles_n) * BN;
 
-  // LDS-DMA sources / destinations.  Half-tile h of A = tile rows {s*WTM + h*QM + [0, QM)} for
-  // s < WM, i.e. BM/16 blocks of 8 rows; wave w loads blocks w*A_INS + i.  Same for B with
-  // (WN, WTN, QN).  Loads are buffer_load ... lds through a buffer descriptor sized to the operand:
-  // rows past M (N) read as zero (no clamping, no per-lane pointers); the per-lane byte offset is
-  // shared by every load of an operand and the row/K position goes in the scalar offset.
-  const int lrow = lane >> 3;
-  const int lchunk = (lane & 7) ^ lrow;  // source pre-swizzled: LDS chunk c of row r holds chunk c ^ (r & 7)
+  // LDS-DMA: instruction covers 16 rows x 64 B; lane l -> row (l >> 2), chunk (l & 3), whose source
+  // chunk is pre-swizzled; rows past M (N) read as zero through the buffer descriptor's range.
+  const int src_chunk = (lane & 3) ^ ((-(lane >> 4)) & 3);
   const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
       (void*)g.A, 0, (int)(((int64_t)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t b_rsrc = __builtin_amdgcn_make_buffer_rsrc(
       (void*)g.B, 0, (int)(((int64_t)(g.N - 1) * g.ldb + g.K) * 2), 0x00020000);
-  const int a_voff = (lrow * (int)g.lda + lchunk * 8) * 2;
-  const int b_voff = (lrow * (int)g.ldb + lchunk * 8) * 2;
-  auto a_row = [&](int h, int i) {  // first tile row of this wave's i-th block of A half-tile h
-    const int blk = wid * A_INS + i;
-    return (blk / (QM / 8)) * WTM + h * QM + (blk % (QM / 8)) * 8;
-  };
-  auto b_row = [&](int h, int i) {
-    const int blk = wid * B_INS + i;
-    return (blk / (QN / 8)) * WTN + h * QN + (blk % (QN / 8)) * 8;
-  };
-  auto load_a = [&](int buf, int h, int k0) {
+  const int a_voff = ((lane >> 2) * (int)g.lda + src_chunk * 8) * 2;
+  const int b_voff = ((lane >> 2) * (int)g.ldb + src_chunk * 8) * 2;
+  auto slot = [&](int seq) { return lds + (seq % NSLOT) * SLOT; };
+  // issue half-tile h (0: A k0, 1: B k0, 2: A k1, 3: B k1) of K-tile kt
+  auto issue = [&](int kt, int h) {
+    f16* dst = slot(4 * kt + h);
+    const int kofs = kt * BK + HK * (h >> 1);
+    if ((h & 1) == 0) {
 #pragma unroll
-    for (int i = 0; i < A_INS; ++i) {
-      const int row = a_row(h, i);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(lds + buf * BUF + row * BK), 16, a_voff,
-                                               (int)(((int64_t)(m0 + row) * g.lda + k0) * 2), 0, 0);
-    }
-  };
-  auto load_b = [&](int buf, int h, int k0) {
+      for (int i = 0; i < A_INS; ++i) {
+        const int row = (wid * A_INS + i) * 16;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(dst + row * HK), 16, a_voff,
+                                                 (int)(((int64_t)(m0 + row) * g.lda + kofs) * 2), 0, 0);
+      }
+    } else {
 #pragma unroll
-    for (int i = 0; i < B_INS; ++i) {
-      const int row = b_row(h, i);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_ptr_t)(lds + buf * BUF + BM * BK + row * BK), 16, b_voff,
-                                               (int)(((int64_t)(n0 + row) * g.ldb + k0) * 2), 0, 0);
+      for (int i = 0; i < B_INS; ++i) {
+        const int row = (wid * B_INS + i) * 16;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_ptr_t)(dst + row * HK), 16, b_voff,
+                                                 (int)(((int64_t)(n0 + row) * g.ldb + kofs) * 2), 0, 0);
+      }
     }
   };
 
-  constexpr int TM = 2 * QTM, TN = 2 * QTN;
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -435,101 +444,84 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fg = lane >> 4;
-  auto read_a = [&](f16x8 (&af)[2][QTM], const f16* base, int mh) {
+  // fragment (row, k 8*fg..8*fg+7 of the k-sub) of a [rows][32] image: row = base16 + fr
+  const int frag_off = fr * HK + ((fg ^ ((-(fr >> 2)) & 3)) << 3);
+  auto read_a = [&](f16x8 (&af)[QTM], const f16* img, int mh) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < QTM; ++i) {
-        const int row = wm * WTM + mh * QM + i * 16 + fr;
-        af[s][i] = *(const f16x8*)(base + row * BK + swz(row, 4 * s + fg) * 8);
-      }
+    for (int i = 0; i < QTM; ++i) af[i] = *(const f16x8*)(img + (wm * WTM + mh * QM + i * 16) * HK + frag_off);
   };
-  auto read_b = [&](f16x8 (&bf)[2][QTN], const f16* base, int nh) {
+  auto read_b = [&](f16x8 (&bf)[TN], const f16* img) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int j = 0; j < QTN; ++j) {
-        const int row = wn * WTN + nh * QN + j * 16 + fr;
-        bf[s][j] = *(const f16x8*)(base + BM * BK + row * BK + swz(row, 4 * s + fg) * 8);
-      }
+    for (int j = 0; j < TN; ++j) bf[j] = *(const f16x8*)(img + (wn * WTN + j * 16) * HK + frag_off);
   };
-  auto mma = [&](const f16x8 (&af)[2][QTM], const f16x8 (&bf)[2][QTN], int mh, int nh) {
+  auto mma = [&](const f16x8 (&af)[QTM], const f16x8 (&bf)[TN], int mh) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int i = 0; i < QTM; ++i)
 #pragma unroll
-      for (int i = 0; i < QTM; ++i)
-#pragma unroll
-        for (int j = 0; j < QTN; ++j)
-          acc[mh * QTM + i][nh * QTN + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[s][j], af[s][i], acc[mh * QTM + i][nh * QTN + j], 0, 0, 0);
+      for (int j = 0; j < TN; ++j)
+        acc[mh * QTM + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[mh * QTM + i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
+  const int nk = g.K / BK;  // >= 2 (the launcher routes K = 64 elsewhere)
   MF_STAMP(0);
-  const int nk = g.K / BK;
-  // prologue: the four half-tiles of K-tile 0 in the order the loop consumes them; retire A0, B0,
-  // B1 and read the fragments of phase 0 (A0, B0)
-  load_a(0, 0, 0);
-  load_b(0, 0, 0);
-  load_b(0, 1, 0);
-  load_a(0, 1, 0);
-  f16x8 fa0[2][QTM], fa1[2][QTM], fb0[2][QTN], fb1[2][QTN];
-  wait_vm_lgkm0<A_INS>();
-  __builtin_amdgcn_s_barrier();
-  read_a(fa0, lds, 0);
-  read_b(fb0, lds, 0);
+  // prologue: K-tiles 0 and 1 (eight half-tiles); retire A k0, B k0 of K-tile 0 and read phase 0's
+  // fragments A(0, k0), B(k0)
+#pragma unroll
+  for (int h = 0; h < 4; ++h) issue(0, h);
+#pragma unroll
+  for (int h = 0; h < 4; ++h) issue(1, h);
+  f16x8 fx[QTM], fy[QTM], fb0[TN], fb1[TN];
+  wait_vm_lgkm0<3 * A_INS + 3 * B_INS>();
+  lds_barrier();
+  read_a(fx, slot(0), 0);
+  read_b(fb0, slot(1));
+  MF_STAMP(1);
 
-  // Phase p of K-tile kt: ds_reads of phase p+1's fragments (their half-tile was retired by the
-  // barrier that opened phase p), one half-tile of glds for K-tile kt+1 (issue order A0 B0 B1 A1),
-  // the MFMAs of phase p on fragments read during phase p-1; then, where phase p+2 reads a new
-  // half-tile, a counted vmcnt + lgkmcnt(0) and a barrier.  Every ds_read of a buffer completes
-  // before the barrier that ends its phase, and a buffer is refilled only in the K-tile after the
-  // one that read it, so all WAR distances are >= 1 barrier.
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cb = kt & 1;
-    const f16* base = lds + cb * BUF;
-    const f16* nbase = lds + (cb ^ 1) * BUF;
-    const bool more = kt + 1 < nk;
-    const int k1 = (kt + 1) * BK;
-    // phase 0: quadrant (0,0); reads B1(kt); retire A1(kt) for phase 1's reads (younger: A0(kt+1))
-    read_b(fb1, base, 1);
-    if (more) load_a(cb ^ 1, 0, k1);
-    mma(fa0, fb0, 0, 0);
-    if (more) wait_vm_lgkm0<A_INS>();
-    else wait_vm_lgkm0<0>();
-    __builtin_amdgcn_s_barrier();
-    // phase 1: quadrant (0,1); reads A1(kt)
-    read_a(fa1, base, 1);
-    if (more) load_b(cb ^ 1, 0, k1);
-    mma(fa0, fb1, 0, 1);
-    // phase 2: quadrant (1,1); re-reads B0(kt); retire A0(kt+1), B0(kt+1) (younger: B1(kt+1))
-    read_b(fb0, base, 0);
-    if (more) {
-      load_b(cb ^ 1, 1, k1);
-      mma(fa1, fb1, 1, 1);
-      wait_vm_lgkm0<B_INS>();
-      __builtin_amdgcn_s_barrier();
-      // phase 3: quadrant (1,0); reads A0(kt+1), B0(kt+1); retire B1(kt+1) (younger: A1(kt+1))
-      f16x8 nb0[2][QTN];
-      read_a(fa0, nbase, 0);
-      read_b(nb0, nbase, 0);
-      load_a(cb ^ 1, 1, k1);
-      mma(fa1, fb0, 1, 0);
-      wait_vm_lgkm0<A_INS>();
-      __builtin_amdgcn_s_barrier();
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < QTN; ++j) fb0[s2][j] = nb0[s2][j];
-    } else {
-      mma(fa1, fb1, 1, 1);
-      mma(fa1, fb0, 1, 0);
+  // one K-tile.  MODE 0: steady state (issues K-tile kt+2);  MODE 1: kt = nk-2 (nothing left to
+  // issue);  MODE 2: kt = nk-1 (the last).  The vmcnt of a retire point = wave instructions issued
+  // after the retired pair.
+  auto ktile = [&](int kt, auto mode_tag) {
+    constexpr int MODE = decltype(mode_tag)::value;
+    const f16* a0 = slot(4 * kt + 0);
+    const f16* a1 = slot(4 * kt + 2);
+    const f16* b1 = slot(4 * kt + 3);
+    // phase 0 (m-half 0, k0): next reads A(1, k0)
+    read_a(fy, a0, 1);
+    if constexpr (MODE == 0) issue(kt + 2, 0);
+    mma(fx, fb0, 0);
+    // retire A k1, B k1 of this K-tile
+    wait_vm_lgkm0<MODE == 0 ? 3 * A_INS + 2 * B_INS : (MODE == 1 ? 2 * A_INS + 2 * B_INS : 0)>();
+    lds_barrier();
+    // phase 1 (m-half 1, k0): next reads A(1, k1), B(k1)
+    read_a(fx, a1, 1);
+    read_b(fb1, b1);
+    if constexpr (MODE == 0) issue(kt + 2, 1);
+    mma(fy, fb0, 1);
+    // phase 2 (m-half 1, k1): next reads A(0, k1)
+    read_a(fy, a1, 0);
+    if constexpr (MODE == 0) issue(kt + 2, 2);
+    mma(fx, fb1, 1);
+    if constexpr (MODE != 2) {
+      // retire A k0, B k0 of the next K-tile
+      wait_vm_lgkm0<MODE == 0 ? 3 * A_INS + 2 * B_INS : A_INS + B_INS>();
+      lds_barrier();
+      // phase 3 (m-half 0, k1): next reads A(0, k0), B(k0) of the next K-tile
+      read_a(fx, slot(4 * kt + 4), 0);
+      read_b(fb0, slot(4 * kt + 5));
+      if constexpr (MODE == 0) issue(kt + 2, 3);
     }
-  }
+    mma(fy, fb1, 0);
+  };
+  for (int kt = 0; kt < nk - 2; ++kt) ktile(kt, std::integral_constant<int, 0>{});
+  ktile(nk - 2, std::integral_constant<int, 1>{});
+  ktile(nk - 1, std::integral_constant<int, 2>{});
+  MF_STAMP(2);
 
   __syncthreads();  // every wave is done with the operand ring (no DMA outstanding after the last K-tile)
   epilogue_store<BM, BN, NT, TM, TN, EPI>(g, lds, acc, m0, n0, wm * WTM, wn * WTN, tid, fr, fg);
+  MF_STAMP(3);
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -586,9 +578,13 @@ extern "C" int mf_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb
   GemmArgs a{(const f16*)A, (const f16*)B, C, (const f16*)bias, (const f16*)aux_in, (f16*)aux_out,
              lda, ldb, ldc, ld_aux, M, N, K, vec8};
   hipStream_t st = (hipStream_t)stream;
-  if (tile == 0) {  // heuristic: fill the 256 CUs
-    int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
-    tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);  // measured: tests/diagnostics/gemm_bench.py
+  if (tile == 0) {  // heuristic: fill the 256 CUs (measured: tests/diagnostics/gemm_bench.py, gemm_stamps.cpp)
+    const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
+    const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
+    if (t256 >= 192 && t256 <= 256 && K >= 512)
+      tile = 20;  // one round of 256x256 tiles on one workgroup per CU (vision QKV: 225 tiles)
+    else
+      tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
   }
   switch (tile) {
     case 1: return launch_tile<128, 128, 2, 2, 2>(a, epilogue, st);
@@ -605,11 +601,11 @@ extern "C" int mf_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb
     case 12: return launch_tile<256, 128, 2, 2, 2>(a, epilogue, st);
     case 13: return launch_tile<128, 256, 2, 2, 3>(a, epilogue, st);
     case 14: return launch_tile<128, 64, 2, 2, 4>(a, epilogue, st);
-    case 20: return launch_tile8<256, 256, 2, 4>(a, epilogue, st);
-    case 21: return launch_tile8<256, 128, 2, 4>(a, epilogue, st);
-    case 22: return launch_tile8<256, 128, 4, 2>(a, epilogue, st);
-    case 23: return launch_tile8<128, 256, 2, 4>(a, epilogue, st);
-    case 24: return launch_tile8<128, 128, 2, 4>(a, epilogue, st);
+    case 20: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 256, 2, 4>(a, epilogue, st);
+    case 21: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 2, 4>(a, epilogue, st);
+    case 22: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 4, 2>(a, epilogue, st);
+    case 23: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<128, 256, 2, 4>(a, epilogue, st);
+    case 24: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<128, 128, 2, 4>(a, epilogue, st);
     default: return mf_set_error("mf_gemm_nt: bad tile id", -2);
   }
 }
