@@ -71,6 +71,20 @@ MF_DEV void stage_wait() {
 
 constexpr float kScale = 0.125f;  // 1/sqrt(64), SDPA default
 
+// In-kernel timeline stamps for diagnostics (tests/diagnostics/attn_stamps.cpp defines
+// MF_ATTN_STAMPS); compiled out of libmapfed.so.
+#ifdef MF_ATTN_STAMPS
+__device__ unsigned long long* g_astamps;
+#define MF_ASTAMP(slot)                                                                   \
+  do {                                                                                    \
+    if (threadIdx.x == 0) g_astamps[(size_t)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define MF_ASTAMP(slot) \
+  do {                  \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------------------------------------
 template <int LKP, bool CAUSAL>
 __global__ __launch_bounds__(512, 4) void attn_fwd_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
@@ -513,6 +527,215 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_dq_kernel(const f16* __restri
   }
 }
 
+// Fused backward, one workgroup per (sequence, head), LP/32 waves, everything for the head in LDS:
+//   phase 0: stage Q and dO (LDS-DMA), D[q] = sum_d dO[q][d] O[q][d] and LSE into LDS;
+//   phase 1: wave w owns keys 32w..32w+31 (K, V fragments in registers) and sweeps the queries:
+//            S^T-ordered P = exp(S*scale - LSE), dS = P (dP - D); dV += P^T dO, dK += dS^T Q, and
+//            dS^T (fp16, the operand precision the dQ product uses) is written to LDS [key][q];
+//   phase 2: K replaces Q in LDS; wave w owns queries 32w..32w+31: dQ = dS K from the stored dS^T
+//            (no recompute of S and dP, no separate D kernel).
+// LDS at LP = 224: Q 28 KB + dO 28 KB + dS^T 224 x 232 fp16 (101.5 KB) + LSE/D 1.75 KB = 159.25 KB.
+template <int LP>
+struct BwdLds {
+  static constexpr int P = LP + 8;  // dS^T row pitch (elements)
+  static constexpr int ELEMS = 2 * LP * 64 + LP * P + 2 * LP * 2;  // fp16 units (LSE, D as 2 fp16 each)
+};
+
+// 16 lanes of a group read rows r0..r0+3 x cols c0..c0+15 of a plain [rows][pitch] fp16 image;
+// lane i of the group gets column c0+i (rows r0..r0+3 in its 4 elements)
+MF_DEV f16x4 tr_read_p(const f16* img, int pitch, int r0, int c0, int lane) {
+  const int ii = lane & 15;
+  const f16* p = img + (r0 + (ii >> 2)) * pitch + c0 + 4 * (ii & 3);
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+  return __builtin_bit_cast(f16x4, v);
+}
+
+template <int LP, bool CAUSAL, int KT>
+__global__ __launch_bounds__(64 * (LP / (16 * KT))) void attn_bwd_fused_kernel(
+    const f16* __restrict__ qkv, int64_t ld_qkv, const f16* __restrict__ out, int64_t ld_out,
+    const f16* __restrict__ dout, int64_t ld_dout, const float* __restrict__ lse, int ld_lse,
+    f16* __restrict__ dqkv, int64_t ld_dqkv, int L, int H) {
+  constexpr int PT = BwdLds<LP>::P;
+  __shared__ __attribute__((aligned(16))) f16 smem[BwdLds<LP>::ELEMS];
+  f16* sQ = smem;                     // [LP][64] swizzled (phase 2: K)
+  f16* sdO = smem + LP * 64;          // [LP][64] swizzled
+  f16* sdST = smem + 2 * LP * 64;     // [LP keys][PT] plain
+  float* sL = (float*)(sdST + LP * PT);
+  float* sD = sL + LP;
+
+  const int D = H * 64;
+  const int nh = blockIdx.x, n = nh / H, h = nh % H;
+  const f16* base = qkv + (int64_t)n * L * ld_qkv;
+  const f16* obase = out + (int64_t)n * L * ld_out;
+  const f16* dobase = dout + (int64_t)n * L * ld_dout;
+  MF_ASTAMP(0);
+  stage_rows<LP>(sQ, base, ld_qkv, L, h * 64);
+  stage_rows<LP>(sdO, dobase, ld_dout, L, h * 64);
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  // phase 0: D and LSE of queries 16*KT*w .. +16*KT-1 (LPQ lanes per query, 64/LPQ dims each)
+  {
+    constexpr int LPQ = 4 / KT, DPL = 64 / LPQ;
+    const int q = 16 * KT * w + lane / LPQ;
+    const int part = lane % LPQ;
+    float d = 0.f;
+    if (q < L) {
+      const f16* o = obase + (int64_t)q * ld_out + h * 64 + DPL * part;
+      const f16* g = dobase + (int64_t)q * ld_dout + h * 64 + DPL * part;
+#pragma unroll
+      for (int c = 0; c < DPL / 8; ++c) {
+        f16x8 a = *(const f16x8*)(o + 8 * c), b = *(const f16x8*)(g + 8 * c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += (float)a[e] * (float)b[e];
+      }
+    }
+#pragma unroll
+    for (int o2 = 1; o2 < LPQ; o2 <<= 1) d += __shfl_xor(d, o2, 64);
+    if (part == 0) {
+      sD[q] = q < L ? d : 0.f;
+      // LSE in base 2 (P = exp2(S * scale * log2e - LSE * log2e)); +inf masks padded queries
+      sL[q] = q < L ? lse[(int64_t)nh * ld_lse + q] * 1.4426950408889634f : INFINITY;
+    }
+  }
+  // the wave's keys: K and V fragments straight to registers
+  const int k0 = 16 * KT * w;
+  f16x8 kf[KT][2], vf[KT][2];
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    const int key = k0 + 16 * kt + fr;
+    const int kc = key < L ? key : L - 1;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      kf[kt][s2] = *(const f16x8*)(base + (int64_t)kc * ld_qkv + D + h * 64 + 32 * s2 + 8 * fg);
+      vf[kt][s2] = *(const f16x8*)(base + (int64_t)kc * ld_qkv + 2 * D + h * 64 + 32 * s2 + 8 * fg);
+    }
+  }
+  stage_wait();  // Q, dO landed; D, LSE visible
+  MF_ASTAMP(1);
+
+  // ---- phase 1: dK, dV for keys k0..k0+31; dS^T -> LDS
+  f32x4 dv[KT][4], dk[KT][4];
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dv[kt][dt] = dk[kt][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int qp = 0; qp < LP / 32; ++qp) {
+    if (CAUSAL && 32 * qp + 31 < k0) continue;  // (KT = 1 waves: k0 may sit mid-block)  // every query of the block precedes every key of the wave
+    f16x8 pf[KT], dsf[KT];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int qt = 2 * qp + a;
+      f32x4 sacc[KT], pacc[KT];
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) sacc[kt] = pacc[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const f16x8 qfr = ld_frag(sQ, qt * 16 + fr, 4 * s2 + fg);
+        const f16x8 ofr = ld_frag(sdO, qt * 16 + fr, 4 * s2 + fg);
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) {
+          sacc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qfr, kf[kt][s2], sacc[kt], 0, 0, 0);
+          pacc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ofr, vf[kt][s2], pacc[kt], 0, 0, 0);
+        }
+      }
+      // the lane's 4 queries are consecutive: one 16-byte LDS read each for LSE and D
+      const f32x4 l4 = *(const f32x4*)(sL + qt * 16 + 4 * fg);
+      const f32x4 d4 = *(const f32x4*)(sD + qt * 16 + 4 * fg);
+      constexpr float kScaleLog2e = 0.125f * 1.4426950408889634f;
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        const int key = k0 + 16 * kt + fr;
+        f16x4 dst;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qq = qt * 16 + 4 * fg + i;
+          const bool valid = key < L && !(CAUSAL && key > qq);  // qq >= L: LSE = +inf -> p = 0
+          const float p = valid ? __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kt][i], kScaleLog2e, -l4[i])) : 0.f;
+          const float ds = p * (pacc[kt][i] - d4[i]);
+          pf[kt][a * 4 + i] = (f16)p;
+          dsf[kt][a * 4 + i] = (f16)ds;
+          dst[i] = (f16)ds;
+        }
+        *(f16x4*)(sdST + (k0 + 16 * kt + fr) * PT + qt * 16 + 4 * fg) = dst;
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const f16x8 ao = cat8(tr_read(sdO, 32 * qp + 4 * fg, 16 * dt, lane), tr_read(sdO, 32 * qp + 16 + 4 * fg, 16 * dt, lane));
+      const f16x8 aq = cat8(tr_read(sQ, 32 * qp + 4 * fg, 16 * dt, lane), tr_read(sQ, 32 * qp + 16 + 4 * fg, 16 * dt, lane));
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        dv[kt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ao, pf[kt], dv[kt][dt], 0, 0, 0);
+        dk[kt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aq, dsf[kt], dk[kt][dt], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    const int key = k0 + 16 * kt + fr;
+    if (key < L) {
+      f16* row = dqkv + ((int64_t)n * L + key) * ld_dqkv + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        f16x4 ok, ov;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          ok[i] = (f16)(dk[kt][dt][i] * kScale);
+          ov[i] = (f16)dv[kt][dt][i];
+        }
+        *(f16x4*)(row + D + 16 * dt + 4 * fg) = ok;
+        *(f16x4*)(row + 2 * D + 16 * dt + 4 * fg) = ov;
+      }
+    }
+  }
+
+  MF_ASTAMP(2);
+  // ---- phase 2: K into the Q region; dQ for queries q0..q0+16*KT-1 from dS^T
+  __syncthreads();  // dS^T complete, every wave done reading Q / dO
+  stage_rows<LP>(sQ, base, ld_qkv, L, D + h * 64);
+  stage_wait();
+  MF_ASTAMP(3);
+  const f16* sK = sQ;
+  const int q0 = 16 * KT * w;
+  f32x4 dq[KT][4];
+#pragma unroll
+  for (int qt = 0; qt < KT; ++qt)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[qt][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int ks = 0; ks < LP / 32; ++ks) {
+    if (CAUSAL && 32 * ks > q0 + 16 * KT - 1) break;
+    f16x8 dsf[KT];
+#pragma unroll
+    for (int qt = 0; qt < KT; ++qt)
+      dsf[qt] = cat8(tr_read_p(sdST, PT, 32 * ks + 4 * fg, q0 + 16 * qt, lane),
+                     tr_read_p(sdST, PT, 32 * ks + 16 + 4 * fg, q0 + 16 * qt, lane));
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const f16x8 ak = cat8(tr_read(sK, 32 * ks + 4 * fg, 16 * dt, lane), tr_read(sK, 32 * ks + 16 + 4 * fg, 16 * dt, lane));
+#pragma unroll
+      for (int qt = 0; qt < KT; ++qt) dq[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ak, dsf[qt], dq[qt][dt], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int qt = 0; qt < KT; ++qt) {
+    const int q = q0 + 16 * qt + fr;
+    if (q < L) {
+      f16* row = dqkv + ((int64_t)n * L + q) * ld_dqkv + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        f16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (f16)(dq[qt][dt][i] * kScale);
+        *(f16x4*)(row + 16 * dt + 4 * fg) = o;
+      }
+    }
+  }
+  MF_ASTAMP(4);
+}
+
 #define MF_ATTN_DISPATCH(LP, CALL)                         \
   switch (LP) {                                            \
     case 32: CALL(32); break;                              \
@@ -582,6 +805,39 @@ extern "C" int mf_attention_bwd(const void* qkv, int64_t ld_qkv, const void* out
   if (ld_lse < L || (ld_qkv % 8) || (ld_dout % 8) || (ld_dqkv % 4)) return mf_set_error("mf_attention_bwd: bad strides", -1);
   const int LP = padded_len(L);
   hipStream_t st = (hipStream_t)stream;
+  static const int bwd_variant = getenv("MAPFED_ATTN_BWD") ? atoi(getenv("MAPFED_ATTN_BWD")) : 2;  // A/B knob
+  if (bwd_variant == 2 && LP <= 224) {
+    static const int kt_w = getenv("MAPFED_ATTN_BWD_KT") ? atoi(getenv("MAPFED_ATTN_BWD_KT")) : 1;  // tuning knob
+    const dim3 gridf(N * H), blockf(64 * (LP / (16 * kt_w)));
+#define CALLBF(P)                                                                                                  \
+  if (causal)                                                                                                      \
+    if (kt_w == 1) attn_bwd_fused_kernel<P, true, 1><<<gridf, blockf, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)out, ld_out, \
+                                                              (const f16*)dout, ld_dout, lse, ld_lse, (f16*)dqkv,   \
+                                                              ld_dqkv, L, H);                                      \
+    else attn_bwd_fused_kernel<P, true, 2><<<gridf, blockf, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)out, ld_out,     \
+                                                              (const f16*)dout, ld_dout, lse, ld_lse, (f16*)dqkv,   \
+                                                              ld_dqkv, L, H);                                      \
+  else                                                                                                             \
+    if (kt_w == 1) attn_bwd_fused_kernel<P, false, 1><<<gridf, blockf, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)out, ld_out, \
+                                                               (const f16*)dout, ld_dout, lse, ld_lse, (f16*)dqkv,  \
+                                                               ld_dqkv, L, H);                                     \
+    else attn_bwd_fused_kernel<P, false, 2><<<gridf, blockf, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)out, ld_out,    \
+                                                               (const f16*)dout, ld_dout, lse, ld_lse, (f16*)dqkv,  \
+                                                               ld_dqkv, L, H);
+    switch (LP) {
+      case 32: CALLBF(32); break;
+      case 64: CALLBF(64); break;
+      case 96: CALLBF(96); break;
+      case 128: CALLBF(128); break;
+      case 160: CALLBF(160); break;
+      case 192: CALLBF(192); break;
+      case 224: CALLBF(224); break;
+      default: return mf_set_error("attention: bad padded length", -1);
+    }
+#undef CALLBF
+    MF_CHECK_LAUNCH();
+    return 0;
+  }
   const int64_t tot = (int64_t)N * H * L;
   attn_bwd_dot_kernel<<<(tot + 255) / 256, 256, 0, st>>>((const f16*)out, ld_out, (const f16*)dout, ld_dout,
                                                         dq_dot_ws, ld_lse, N, L, H);
