@@ -17,6 +17,7 @@ P, I, L, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 SIGNATURES = {
     "mf_abi_version": [],
     "mf_gemm_nt": [P, L, P, L, P, L, I, I, I, P, P, P, L, I, I, P],
+    "mf_gemm": [P, L, I, P, L, I, P, L, I, I, I, P, P, P, L, I, I, P],
     "mf_layernorm_fwd": [P, L, P, P, P, P, L, P, P, I, I, P],
     "mf_layernorm_bwd_blocks": [I],
     "mf_layernorm_bwd": [P, L, P, L, P, P, P, P, P, L, P, L, P, P, P, I, I, I, P],

@@ -229,21 +229,86 @@ MF_DEV void epilogue_store(const GemmArgs& g, f16* lds, const f32x4 (&acc)[TM][T
 }
 
 // Tile BM x BN, (WM x WN) waves each owning a (BM/WM) x (BN/WN) block of 16x16 MFMA tiles, BK = 64.
-// Operands go HBM -> LDS by global_load_lds (16 B per lane, no VGPR round trip): each wave
-// instruction fills 8 rows x 128 B of the [rows][64] fp16 image; the 16-B-chunk XOR swizzle
-// (chunk ^ (row & 7)) is applied to the per-lane SOURCE address (the LDS side is lane-linear), so
-// the ds_read_b128 fragment reads stay conflict-free.  Two LDS buffers: the loads of K-step t+1
-// are issued before the fragment reads + MFMAs of step t and drained by one vmcnt(0) + barrier
-// per step (cdna_hip_programming.md §5.5 T3/T4 minimum 2-phase form).
-template <int BM, int BN, int WM, int WN, int S, int EPI, bool PRIO = false>
+// Operands go HBM -> LDS by LDS-DMA (buffer_load ... lds, 16 B per lane, no VGPR round trip) through
+// buffer descriptors sized to the operand, so rows past M / N (and, for K-major operands, k-rows
+// past K) read as zero: no clamping and no K padding.  Two layouts per operand:
+//   * row-major [rows][K] (TA/TB false, nn.Linear weights, activations): each wave instruction fills
+//     8 rows x 128 B of a [rows][64] image whose 16-B chunk c of row r holds chunk c ^ (r & 7);
+//     fragments by ds_read_b128;
+//   * K-major [K][rows] (TA/TB true: dY^T / X of the weight gradients, W as [in] x [out] of the dX
+//     products): each instruction fills 512/R k-rows x 2R bytes of a [64][R] image whose 16-B chunk c
+//     of k-row k holds chunk c ^ fT(k); fragments by two ds_read_b64_tr_b16 (4 k each, hardware
+//     transpose), conflict-free (bank model in the commit history of this file).
+// The swizzles are applied to the per-lane SOURCE address (the LDS side of an LDS-DMA is lane-linear).
+// Two LDS buffers: the loads of K-step t+1 are issued before the fragment reads + MFMAs of step t and
+// drained by one vmcnt(0) + barrier per step (cdna_hip_programming.md §5.5 T3/T4 minimum 2-phase form).
+template <int R>
+MF_DEV int swz_t(int k) {  // 16-byte-chunk XOR of a K-major image with R fp16 per k-row
+  if constexpr (R == 128) return 2 * ((k & 3) | (((k >> 3) & 1) << 2));
+  else return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+}
+
+// 16 k-values (k0 .. k0+7 of column c) of a K-major [64][R] image as one MFMA fragment
+template <int R>
+MF_DEV f16x8 frag_t(const f16* img, int kr0, int c0, int fr) {
+  f16x4 h[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int k = kr0 + 4 * u + (fr >> 2);
+    const int col = c0 + 4 * (fr & 3);
+    const f16* p = img + k * R + ((((col >> 3) ^ swz_t<R>(k))) << 3) + (col & 7);
+    s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+    h[u] = __builtin_bit_cast(f16x4, v);
+  }
+  return (f16x8){h[0][0], h[0][1], h[0][2], h[0][3], h[1][0], h[1][1], h[1][2], h[1][3]};
+}
+
+// LDS-DMA source offset (bytes, k0 = 0) of this lane's 16 B for wave instruction ins_i, and the
+// instruction's element offset in the operand image: row-major [rows][64] or K-major [64][RW]
+template <bool T, int RW>
+MF_DEV void dma_setup(int lane, int wid, int64_t ld, int row0, int ins_i, int nins, int& voff, int& dst) {
+  if constexpr (!T) {
+    const int lrow = lane >> 3, lchunk = (lane & 7) ^ lrow;
+    const int brow = (wid * nins + ins_i) * 8;
+    voff = (int)((((int64_t)(row0 + brow + lrow)) * ld + lchunk * 8) * 2);
+    dst = brow * BK;
+  } else {
+    constexpr int CPR = RW / 8;   // 16-B chunks per k-row
+    constexpr int KR = 512 / RW;  // k-rows per instruction
+    const int kbase = (wid * nins + ins_i) * KR;
+    const int kr = kbase + lane / CPR;
+    const int c = (lane % CPR) ^ swz_t<RW>(kr);
+    voff = (int)(((int64_t)kr * ld + row0 + c * 8) * 2);
+    dst = kbase * RW;
+  }
+}
+
+// issue one stage's LDS-DMA (all offsets in the range-checked VGPR offset).  The buffer descriptors
+// are built here from (pointer, byte range): a descriptor-typed parameter fails template
+// substitution in hipcc's host pass, which silently drops the kernel's host stub.
+template <int A_INS, int B_INS>
+MF_DEV void dma_stage(const f16* A, int a_bytes, const f16* B, int b_bytes, f16* la, f16* lb,
+                      const int* a_voff, const int* a_dst, const int* b_voff, const int* b_dst, int a_k, int b_k) {
+  const auto a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, a_bytes, 0x00020000);
+  const auto b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, b_bytes, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < A_INS; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(la + a_dst[i]), 16, a_voff[i] + a_k, 0, 0, 0);
+#pragma unroll
+  for (int i = 0; i < B_INS; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_ptr_t)(lb + b_dst[i]), 16, b_voff[i] + b_k, 0, 0, 0);
+}
+
+template <int BM, int BN, int WM, int WN, int S, int EPI, bool TA = false, bool TB = false>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g) {
   constexpr int NW = WM * WN;
   constexpr int NT = NW * 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;  // per-wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int A_INS = BM / 8 / NW;  // glds wave-instructions per stage per wave
+  constexpr int A_INS = BM / 8 / NW;  // LDS-DMA wave-instructions per stage per wave (1 KiB each)
   constexpr int B_INS = BN / 8 / NW;
   static_assert(A_INS * 8 * NW == BM && B_INS * 8 * NW == BN, "tile / wave split");
+  static_assert((!TA || BM == 64 || BM == 128) && (!TB || BN == 64 || BN == 128), "K-major image widths");
   constexpr int STAGE = (BM + BN) * BK;  // fp16 elements per stage
   constexpr int LDS_ELEMS = S * STAGE > BM * (BN + 8) ? S * STAGE : BM * (BN + 8);
   __shared__ __attribute__((aligned(1024))) f16 lds[LDS_ELEMS];
@@ -263,35 +328,22 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g) {
   const int m0 = (wgid / tiles_n) * BM;
   const int n0 = (wgid % tiles_n) * BN;
 
-  // per-lane glds sources: instruction i of this wave covers tile rows (wid*A_INS + i)*8 + lane/8
-  const int lrow = lane >> 3;
-  const int lchunk = (lane & 7) ^ lrow;  // pre-swizzled source chunk (row & 7 == lrow)
-  const f16* a_src[A_INS];
-  const f16* b_src[B_INS];
+  // per-operand LDS-DMA: byte offset of this lane's 16 B for instruction i at k0 = 0 (all offsets in
+  // the VGPR offset: the descriptor's range check covers it), and the instruction's LDS destination
+  const int a_bytes = (int)((TA ? (int64_t)(g.K - 1) * g.lda + g.M : (int64_t)(g.M - 1) * g.lda + g.K) * 2);
+  const int b_bytes = (int)((TB ? (int64_t)(g.K - 1) * g.ldb + g.N : (int64_t)(g.N - 1) * g.ldb + g.K) * 2);
+  int a_voff[A_INS], a_dst[A_INS], b_voff[B_INS], b_dst[B_INS];
 #pragma unroll
-  for (int i = 0; i < A_INS; ++i) {
-    int row = m0 + (wid * A_INS + i) * 8 + lrow;
-    row = row < g.M ? row : g.M - 1;
-    a_src[i] = g.A + (int64_t)row * g.lda + lchunk * 8;
-  }
+  for (int i = 0; i < A_INS; ++i) dma_setup<TA, BM>(lane, wid, g.lda, m0, i, A_INS, a_voff[i], a_dst[i]);
 #pragma unroll
-  for (int i = 0; i < B_INS; ++i) {
-    int row = n0 + (wid * B_INS + i) * 8 + lrow;
-    row = row < g.N ? row : g.N - 1;
-    b_src[i] = g.B + (int64_t)row * g.ldb + lchunk * 8;
-  }
-  auto stage = [&](int buf, int k0) {
-    f16* la = lds + buf * STAGE;
-    f16* lb = la + BM * BK;
-#pragma unroll
-    for (int i = 0; i < A_INS; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + k0),
-                                       (lds_ptr_t)(la + (wid * A_INS + i) * 8 * BK), 16, 0, 0);
-#pragma unroll
-    for (int i = 0; i < B_INS; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + k0),
-                                       (lds_ptr_t)(lb + (wid * B_INS + i) * 8 * BK), 16, 0, 0);
-  };
+  for (int i = 0; i < B_INS; ++i) dma_setup<TB, BN>(lane, wid, g.ldb, n0, i, B_INS, b_voff[i], b_dst[i]);
+  // K step k0 advances a row-major operand by k0 elements, a K-major one by k0 k-rows
+  const int a_kstep = TA ? (int)(g.lda * 2) : 2, b_kstep = TB ? (int)(g.ldb * 2) : 2;
+#define MF_STAGE(buf, k0)                                                                                     \
+  dma_stage<A_INS, B_INS>(g.A, a_bytes, g.B, b_bytes, lds + (buf)*STAGE, lds + (buf)*STAGE + BM * BK, a_voff, a_dst, \
+                          b_voff, b_dst, (k0)*a_kstep, (k0)*b_kstep)
+
+
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -300,11 +352,11 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g) {
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   MF_STAMP(0);
-  const int nk = g.K / BK;
+  const int nk = (g.K + BK - 1) / BK;  // a ragged last K step only with both operands K-major (zero-filled)
   // prologue: S-1 stages in flight
 #pragma unroll
   for (int p = 0; p < S - 1; ++p)
-    if (p < nk) stage(p, p * BK);
+    if (p < nk) MF_STAGE(p, p * BK);
 
   const int fr = lane & 15, fg = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
@@ -320,7 +372,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g) {
     }
     __builtin_amdgcn_s_barrier();
     if (kt == 0) MF_STAMP(1);
-    if (kt + S - 1 < nk) stage((kt + S - 1) % S, (kt + S - 1) * BK);
+    if (kt + S - 1 < nk) MF_STAGE((kt + S - 1) % S, (kt + S - 1) * BK);
     const f16* la = lds + (kt % S) * STAGE;
     const f16* lb = la + BM * BK;
     // fragments of sub-step 1 are read while the MFMAs of sub-step 0 run (register double buffer)
@@ -330,15 +382,20 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wave_m * WTM + i * 16 + fr;
-        af[s][i] = *(const f16x8*)(la + row * BK + swz(row, 4 * s + fg) * 8);
+        if constexpr (TA)
+          af[s][i] = frag_t<BM>(la, 32 * s + 8 * fg, wave_m * WTM + i * 16, fr);
+        else
+          af[s][i] = *(const f16x8*)(la + row * BK + swz(row, 4 * s + fg) * 8);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wave_n * WTN + j * 16 + fr;
-        bf[s][j] = *(const f16x8*)(lb + row * BK + swz(row, 4 * s + fg) * 8);
+        if constexpr (TB)
+          bf[s][j] = frag_t<BN>(lb, 32 * s + 8 * fg, wave_n * WTN + j * 16, fr);
+        else
+          bf[s][j] = *(const f16x8*)(lb + row * BK + swz(row, 4 * s + fg) * 8);
       }
     }
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -346,9 +403,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[s][j], af[s][i], acc[i][j], 0, 0, 0);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   }
 
+#undef MF_STAGE
   // epilogue.  lane holds C[m = .. + fr][n = .. + 4*fg + e], e = 0..3.
   MF_STAMP(2);
   __syncthreads();  // every wave is done with the operand ring
@@ -407,7 +464,8 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   const int n0 = (wgid % tiles_n) * BN;
 
   // LDS-DMA: instruction covers 16 rows x 64 B; lane l -> row (l >> 2), chunk (l & 3), whose source
-  // chunk is pre-swizzled; rows past M (N) read as zero through the buffer descriptor's range.
+  // chunk is pre-swizzled; rows past M (N) read as zero through the buffer descriptor's range (every
+  // offset is in the range-checked VGPR offset, none in the scalar offset).
   const int src_chunk = (lane & 3) ^ ((-(lane >> 4)) & 3);
   const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
       (void*)g.A, 0, (int)(((int64_t)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
@@ -424,15 +482,15 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < A_INS; ++i) {
         const int row = (wid * A_INS + i) * 16;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(dst + row * HK), 16, a_voff,
-                                                 (int)(((int64_t)(m0 + row) * g.lda + kofs) * 2), 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(dst + row * HK), 16,
+                                                 a_voff + (int)(((int64_t)(m0 + row) * g.lda + kofs) * 2), 0, 0, 0);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < B_INS; ++i) {
         const int row = (wid * B_INS + i) * 16;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_ptr_t)(dst + row * HK), 16, b_voff,
-                                                 (int)(((int64_t)(n0 + row) * g.ldb + kofs) * 2), 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_ptr_t)(dst + row * HK), 16,
+                                                 b_voff + (int)(((int64_t)(n0 + row) * g.ldb + kofs) * 2), 0, 0, 0);
       }
     }
   };
@@ -542,44 +600,73 @@ int launch_tile8(const GemmArgs& a, int epi, hipStream_t st) {
   return 0;
 }
 
-template <int BM, int BN, int WM, int WN, int S>
+template <int BM, int BN, int WM, int WN, int S, bool TA = false, bool TB = false>
 int launch_tile(const GemmArgs& a, int epi, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles), block(WM * WN * 64);
   switch (epi) {
-    case EPI_NONE: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_NONE><<<grid, block, 0, st>>>(a); break;
-    case EPI_BIAS: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_BIAS><<<grid, block, 0, st>>>(a); break;
-    case EPI_BIAS_RESID: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_BIAS_RESID><<<grid, block, 0, st>>>(a); break;
-    case EPI_BIAS_GELU: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_BIAS_GELU><<<grid, block, 0, st>>>(a); break;
-    case EPI_DGELU: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_DGELU><<<grid, block, 0, st>>>(a); break;
-    case EPI_F32: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_F32><<<grid, block, 0, st>>>(a); break;
-    case EPI_RESID: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_RESID><<<grid, block, 0, st>>>(a); break;
-    default: return mf_set_error("mf_gemm_nt: bad epilogue", -2);
+    case EPI_NONE: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_NONE, TA, TB><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_BIAS, TA, TB><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_RESID: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_BIAS_RESID, TA, TB><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_GELU: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_BIAS_GELU, TA, TB><<<grid, block, 0, st>>>(a); break;
+    case EPI_DGELU: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_DGELU, TA, TB><<<grid, block, 0, st>>>(a); break;
+    case EPI_F32: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_F32, TA, TB><<<grid, block, 0, st>>>(a); break;
+    case EPI_RESID: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_RESID, TA, TB><<<grid, block, 0, st>>>(a); break;
+    default: return mf_set_error("mf_gemm: bad epilogue", -2);
   }
   MF_CHECK_LAUNCH();
   return 0;
 }
 
+// K-major operand combinations run on the 4-wave kernel's 128x128 / 128x64 / 64x64 tiles (a plain
+// function: kernel templates instantiated only through nested function templates lose their host
+// stubs under hipcc)
+int launch_kmajor(const GemmArgs& a, bool ta, bool tb, int epi, int tile, hipStream_t st) {
+#define MF_KM(TA_, TB_)                                                             \
+  switch (tile) {                                                                   \
+    case 1: return launch_tile<128, 128, 2, 2, 2, TA_, TB_>(a, epi, st);            \
+    case 2: return launch_tile<128, 64, 2, 2, 2, TA_, TB_>(a, epi, st);             \
+    case 3: return launch_tile<64, 64, 2, 2, 2, TA_, TB_>(a, epi, st);              \
+    default: return mf_set_error("mf_gemm: K-major operands need tile 0-3", -2);    \
+  }
+  if (ta && tb) { MF_KM(true, true) }
+  if (ta) { MF_KM(true, false) }
+  MF_KM(false, true)
+#undef MF_KM
+}
+
 }  // namespace
 
-extern "C" int mf_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M,
-                          int N, int K, const void* bias, const void* aux_in, void* aux_out, int64_t ld_aux,
-                          int epilogue, int tile, void* stream) {
+// C[M,N] = epilogue(op(A) . op(B)^T):  a_kmajor = 0: A[m][k] at A[m*lda + k], 1: A[k*lda + m];
+// b_kmajor = 0: B[n][k] at B[n*ldb + k], 1: B[k*ldb + n].
+extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb, int b_kmajor, void* C,
+                       int64_t ldc, int M, int N, int K, const void* bias, const void* aux_in, void* aux_out,
+                       int64_t ld_aux, int epilogue, int tile, void* stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (K <= 0 || (K % BK) != 0) return mf_set_error("mf_gemm_nt: K must be a positive multiple of 64", -1);
-  if ((N % 4) != 0 || (lda % 8) || (ldb % 8) || (ldc % 4)) return mf_set_error("mf_gemm_nt: alignment", -1);
+  const bool both_k = a_kmajor && b_kmajor;
+  if (K <= 0 || (!both_k && (K % BK) != 0))
+    return mf_set_error("mf_gemm: K must be a positive multiple of 64 unless both operands are K-major", -1);
+  if ((N % 4) != 0 || (lda % 8) || (ldb % 8) || (ldc % 4)) return mf_set_error("mf_gemm: alignment", -1);
+  if ((a_kmajor && (M % 8 || lda < M)) || (b_kmajor && (N % 8 || ldb < N)) || (!a_kmajor && lda < K) ||
+      (!b_kmajor && ldb < K))
+    return mf_set_error("mf_gemm: K-major operands need rows % 8 == 0 and ld >= rows; row-major ld >= K", -1);
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16) return mf_set_error("mf_gemm: operands must be 16-byte aligned", -1);
   if ((epilogue == EPI_BIAS || epilogue == EPI_BIAS_RESID || epilogue == EPI_BIAS_GELU) && !bias)
-    return mf_set_error("mf_gemm_nt: epilogue needs bias", -1);
+    return mf_set_error("mf_gemm: epilogue needs bias", -1);
   if ((epilogue == EPI_BIAS_RESID || epilogue == EPI_DGELU || epilogue == EPI_RESID) && !aux_in)
-    return mf_set_error("mf_gemm_nt: epilogue needs aux_in", -1);
-  if (epilogue == EPI_BIAS_GELU && !aux_out) return mf_set_error("mf_gemm_nt: epilogue needs aux_out", -1);
+    return mf_set_error("mf_gemm: epilogue needs aux_in", -1);
+  if (epilogue == EPI_BIAS_GELU && !aux_out) return mf_set_error("mf_gemm: epilogue needs aux_out", -1);
   const int vec8 = (ldc % 8 == 0) && (ld_aux % 8 == 0) && ((uintptr_t)C % 16 == 0) &&
                    (!aux_in || (uintptr_t)aux_in % 16 == 0) && (!aux_out || (uintptr_t)aux_out % 16 == 0);
   GemmArgs a{(const f16*)A, (const f16*)B, C, (const f16*)bias, (const f16*)aux_in, (f16*)aux_out,
              lda, ldb, ldc, ld_aux, M, N, K, vec8};
   hipStream_t st = (hipStream_t)stream;
+  const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
+  if (a_kmajor || b_kmajor) {
+    if (tile == 0) tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
+    return launch_kmajor(a, a_kmajor != 0, b_kmajor != 0, epilogue, tile, st);
+  }
   if (tile == 0) {  // heuristic: fill the 256 CUs (measured: tests/diagnostics/gemm_bench.py, gemm_stamps.cpp)
-    const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
     const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
     if (t256 >= 192 && t256 <= 256 && K >= 512)
       tile = 20;  // one round of 256x256 tiles on one workgroup per CU (vision QKV: 225 tiles)
@@ -591,21 +678,19 @@ extern "C" int mf_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb
     case 2: return launch_tile<128, 64, 2, 2, 2>(a, epilogue, st);
     case 3: return launch_tile<64, 64, 2, 2, 2>(a, epilogue, st);
     case 4: return launch_tile<256, 128, 4, 2, 2>(a, epilogue, st);
-    case 5: return launch_tile<256, 128, 4, 2, 3>(a, epilogue, st);
     case 6: return launch_tile<128, 128, 2, 2, 3>(a, epilogue, st);
     case 7: return launch_tile<128, 64, 2, 2, 3>(a, epilogue, st);
-    case 8: return launch_tile<128, 256, 2, 4, 3>(a, epilogue, st);
-    case 9: return launch_tile<256, 256, 2, 4, 2>(a, epilogue, st);
-    case 10: return launch_tile<256, 128, 2, 2, 3>(a, epilogue, st);
-    case 11: return launch_tile<128, 128, 2, 2, 4>(a, epilogue, st);
-    case 12: return launch_tile<256, 128, 2, 2, 2>(a, epilogue, st);
-    case 13: return launch_tile<128, 256, 2, 2, 3>(a, epilogue, st);
-    case 14: return launch_tile<128, 64, 2, 2, 4>(a, epilogue, st);
     case 20: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 256, 2, 4>(a, epilogue, st);
     case 21: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 2, 4>(a, epilogue, st);
     case 22: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 4, 2>(a, epilogue, st);
     case 23: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<128, 256, 2, 4>(a, epilogue, st);
     case 24: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<128, 128, 2, 4>(a, epilogue, st);
-    default: return mf_set_error("mf_gemm_nt: bad tile id", -2);
+    default: return mf_set_error("mf_gemm: bad tile id", -2);
   }
+}
+
+extern "C" int mf_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M,
+                          int N, int K, const void* bias, const void* aux_in, void* aux_out, int64_t ld_aux,
+                          int epilogue, int tile, void* stream) {
+  return mf_gemm(A, lda, 0, B, ldb, 0, C, ldc, M, N, K, bias, aux_in, aux_out, ld_aux, epilogue, tile, stream);
 }

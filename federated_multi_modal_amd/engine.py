@@ -155,7 +155,6 @@ class _Tower:
         dev = eng.device
         R = N * L
         self.R = R
-        self.Rp = ((R + 63) // 64) * 64  # padded row count (K dim of the dW GEMMs)
         e = lambda *s, dt=F16: torch.empty(*s, device=dev, dtype=dt)
         self.X = [e(R, D) for _ in range(layers + 1)]
         self.QKV = [e(R, 3 * D) for _ in range(layers)]
@@ -179,9 +178,6 @@ class _Tower:
         self.dF = e(R, 4 * D)
         self.attn_ws = e(N * H * L, dt=F32)
         self.cs_ws = e(ops.colsum_ws_floats(R, 4 * D), dt=F32)
-        # transposed operands of the block-11 weight gradients (zero padded to Rp columns)
-        self.tA = torch.zeros(4 * D, self.Rp, device=dev, dtype=F16)
-        self.tB = torch.zeros(4 * D, self.Rp, device=dev, dtype=F16)
 
     # -- parameters of block i
     def p(self, i: int, key: str) -> torch.Tensor:
@@ -218,12 +214,8 @@ class _Tower:
         # self.H1 / H2 / G now hold the last layer's (block 11) tensors, kept for its dW
 
     def _dw(self, dY: torch.Tensor, Xin: torch.Tensor, dW: torch.Tensor, db: torch.Tensor):
-        """dW[out,in] = dY^T . Xin (fp16 out), db = colsum(dY)."""
-        R, Rp = self.R, self.Rp
-        o, k = dY.shape[1], Xin.shape[1]
-        ops.transpose(dY, self.tA[:o, :R])
-        ops.transpose(Xin, self.tB[:k, :R])
-        ops.gemm_nt(self.tA[:o], self.tB[:k], dW, epilogue=ops.EPI_NONE)
+        """dW[out,in] = dY^T . Xin (fp16 out; both operands read K-major in place, K = rows), db = colsum(dY)."""
+        ops.gemm(dY, Xin, dW, epilogue=ops.EPI_NONE, a_kmajor=True, b_kmajor=True)
         ops.colsum(dY, db, self.cs_ws)
 
     def backward(self, n_prompted: int, prompt_grads: List[torch.Tensor]):
@@ -282,8 +274,7 @@ class MapleEngine:
         else:
             assert shared.K == self.K and shared.J == self.J and shared.device == self.device
             for a in ("n16", "n32", "flat16", "flat32", "gflat16", "gflat32", "mom16", "mom32", "P", "G",
-                      "trainable_names", "conv_w", "chunks", "nchunks", "norm_part", "clip_out", "WT", "projT",
-                      "text_projT", "tokenized", "token_prefix", "token_suffix", "eot_rows", "hyper"):
+                      "trainable_names", "conv_w", "chunks", "nchunks", "norm_part", "clip_out", "WT", "tokenized", "token_prefix", "token_suffix", "eot_rows", "hyper"):
                 setattr(self, a, getattr(shared, a))
         G2 = d.grid * d.grid
         self.Lv = G2 + 1 + cfg.n_ctx
@@ -358,7 +349,10 @@ class MapleEngine:
         self.nchunks = len(rows)
         self.norm_part = torch.empty(self.nchunks, device=dev, dtype=F32)
         self.clip_out = torch.zeros(3, device=dev, dtype=F32)
-        # transposed weight copies for the dX products, and the transposed head projections
+        # W^T copies for the dX products (a row-major B operand keeps them on the fast ds_read_b128
+        # fragment path; measured 15-18 % faster than reading W K-major).  Frozen blocks are transposed
+        # once; block 11 after every optimizer step.  The weight gradients and the head projections
+        # read their operands in place (K-major GEMM operands, mf_gemm).
         self.WT: Dict[str, torch.Tensor] = {}
         for n, s, dt in self.specs:
             if ".resblocks." in n and n.endswith(("in_proj_weight", "out_proj.weight", "c_fc.weight", "c_proj.weight")):
@@ -366,17 +360,10 @@ class MapleEngine:
         self.refresh_transposes(all_layers=True)
 
     def refresh_transposes(self, all_layers: bool = False):
-        """W^T copies feed the dX GEMMs; frozen blocks once, block 11 after every optimizer step."""
+        """W^T copies of the dX products: every block once, block 11 (trainable) after each update."""
         for n, t in self.WT.items():
             if all_layers or ".resblocks.11." in n:
                 ops.transpose(self.P[n], t)
-        if all_layers:  # frozen head projections (x @ proj == NT GEMM with proj^T); in place, so that
-            # pointers captured in a hipGraph stay valid
-            if not hasattr(self, "projT"):
-                self.projT = torch.empty_like(self.P["image_encoder.proj"].t().contiguous())
-                self.text_projT = torch.empty_like(self.P["text_encoder.text_projection"].t().contiguous())
-            ops.transpose(self.P["image_encoder.proj"], self.projT)
-            ops.transpose(self.P["text_encoder.text_projection"], self.text_projT)
 
     def _build_text_constants(self):
         """token prefix / suffix buffers and the EOT gather index (trainers/maple.py:136-149)."""
@@ -498,7 +485,8 @@ class MapleEngine:
         t.forward(self.txt_deep)
         ops.layernorm_fwd(t.X[-1], P["text_encoder.ln_final.weight"], P["text_encoder.ln_final.bias"], self.txt_final,
                           self.fin_mean, self.fin_rstd, row_index=self.eot_rows)
-        ops.gemm_nt(self.txt_final, self.text_projT, self.txt_feat, epilogue=ops.EPI_NONE)
+        ops.gemm(self.txt_final, P["text_encoder.text_projection"], self.txt_feat, epilogue=ops.EPI_NONE,
+                 b_kmajor=True)
 
     def _vision_forward(self):
         P = self.P
@@ -512,7 +500,7 @@ class MapleEngine:
         v.forward(self.vis_deep)
         ops.layernorm_fwd(v.X[-1], P["image_encoder.ln_post.weight"], P["image_encoder.ln_post.bias"], self.vis_post,
                           self.post_mean, self.post_rstd, row_index=self.cls_rows)
-        ops.gemm_nt(self.vis_post, self.projT, self.img_feat, epilogue=ops.EPI_NONE)
+        ops.gemm(self.vis_post, P["image_encoder.proj"], self.img_feat, epilogue=ops.EPI_NONE, b_kmajor=True)
 
     def eval_batch(self, labels: Optional[torch.Tensor], acc: torch.Tensor, pred: Optional[torch.Tensor] = None):
         """One test batch (trainers/maple.py:671-677): logits, argmax, correct count accumulated in

@@ -83,6 +83,28 @@ def gemm_nt(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NON
     return C
 
 
+def gemm(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NONE, tile=0, a_kmajor=False,
+         b_kmajor=False):
+    """C[M,N] = epi(op(A) . op(B)^T): A is [M,K] (or [K,M] when a_kmajor), B is [N,K] (or [K,N]
+    when b_kmajor) -- the K-major forms read dY^T / X / W of the backward products in place."""
+    M, Ka = (A.shape[1], A.shape[0]) if a_kmajor else A.shape
+    N, Kb = (B.shape[1], B.shape[0]) if b_kmajor else B.shape
+    assert Ka == Kb, (A.shape, a_kmajor, B.shape, b_kmajor)
+    K = Ka
+    if C is None:
+        C = torch.empty(M, N, device=A.device, dtype=torch.float32 if epilogue == EPI_F32 else torch.float16)
+    aux = aux_in if aux_in is not None else aux_out
+    ld_aux = _ld(aux) if aux is not None else 0
+    ev = None
+    if _PROBE is not None and _PROBE.kind == "gemm":
+        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N))
+    call("mf_gemm", _p(A), _ld(A), int(a_kmajor), _p(B), _ld(B), int(b_kmajor), _p(C), _ld(C), M, N, K, _p(bias),
+         _p(aux_in), _p(aux_out), ld_aux, epilogue, tile, _s())
+    if ev is not None:
+        ev.record()
+    return C
+
+
 def layernorm_fwd(x, gamma, beta, y=None, mean=None, rstd=None, row_index=None):
     rows = row_index.numel() if row_index is not None else x.shape[0]
     D = x.shape[1]

@@ -38,6 +38,15 @@ int mf_abi_version(void);
 int mf_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
                const void* bias, const void* aux_in, void* aux_out, int64_t ld_aux, int epilogue, int tile,
                void* stream);
+/* General layouts: C[M,N] = epilogue(op(A) . op(B)^T) with
+ *   a_kmajor = 0: A[m][k] at A[m*lda + k]  |  1: A[k*lda + m]   (e.g. dY^T of a weight gradient)
+ *   b_kmajor = 0: B[n][k] at B[n*ldb + k]  |  1: B[k*ldb + n]   (e.g. nn.Linear W [out][in] in dX = dY . W)
+ * K-major operands need rows % 8 == 0; K % 64 == 0 unless both operands are K-major (then any K: the
+ * tail reads as zero).  Replaces the autograd dX / dW products of every nn.Linear on the path
+ * (torch.mm(grad, W), torch.mm(grad^T, X)) without materialising a transpose.                      */
+int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb, int b_kmajor, void* C, int64_t ldc,
+            int M, int N, int K, const void* bias, const void* aux_in, void* aux_out, int64_t ld_aux, int epilogue,
+            int tile, void* stream);
 
 /* ---- LayerNorm (fp16 io, fp32 math; clip/model.py:153-159) --------------------------------
  * row_index (optional, int32): output row i normalises input row row_index[i]

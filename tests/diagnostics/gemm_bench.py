@@ -78,6 +78,28 @@ def main():
             res.append(f"{fl / us / 1e6:7.0f}{'' if ok else '!'}")
         print(f"{name:10s} {fl / ub / 1e6:8.0f} " + " ".join(f"{r:>8s}" for r in res), flush=True)
     print(f"sum over a c4 step: ours (tile {tiles[0]}) {tot_us / 1e3:.2f} ms, hipBLASLt plain {tot_blas / 1e3:.2f} ms")
+    # K-major operand forms (dX = dY . W with W read as [out][in]; dW = dY^T X read in place)
+    print("K-major forms (TFLOP/s): NN = B K-major, TN = both K-major", flush=True)
+    for name, M, N, K, epi, ak, bk in [("v.dfc NN", 6368, 3072, 768, ops.EPI_DGELU, False, True),
+                                       ("v.dh NN", 6368, 768, 3072, ops.EPI_NONE, False, True),
+                                       ("v.dqkv NN", 6368, 768, 2304, ops.EPI_NONE, False, True),
+                                       ("t.dh NN", 2926, 512, 2048, ops.EPI_NONE, False, True),
+                                       ("v.dW_fc TN", 3072, 768, 6368, ops.EPI_NONE, True, True),
+                                       ("v.dW_pr TN", 768, 3072, 6368, ops.EPI_NONE, True, True)]:
+        A = (torch.randn(K, M, device=dev) if ak else torch.randn(M, K, device=dev)).half()
+        B = ((torch.randn(K, N, device=dev) if bk else torch.randn(N, K, device=dev)) * K ** -0.5).half()
+        aux = torch.randn(M, N, device=dev).half()
+        C = torch.empty(M, N, device=dev, dtype=torch.float16)
+        kw = dict(C=C, epilogue=epi, a_kmajor=ak, b_kmajor=bk)
+        if epi == ops.EPI_DGELU:
+            kw["aux_in"] = aux
+        fl = 2 * M * N * K
+        res = []
+        for t in (1, 2, 3):
+            us = timeit(lambda: ops.gemm(A, B, tile=t, **kw))
+            res.append(f"t{t} {fl / us / 1e6:6.0f}")
+        us0 = timeit(lambda: ops.gemm(A, B, tile=0, **kw))
+        print(f"{name:12s} " + "  ".join(res) + f"  auto {fl / us0 / 1e6:6.0f}", flush=True)
 
 
 if __name__ == "__main__":

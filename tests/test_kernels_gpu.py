@@ -51,6 +51,46 @@ def test_gemm_bias(dev, M, N, K, tile):
     torch.testing.assert_close(C32.double(), A.double() @ B.double().t(), rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("M,N,K,ak,bk,tile", [
+    # weight gradients dW[out,in] = dY^T X: both operands K-major, K = rows (ragged: no padding)
+    (3072, 768, 6368, True, True, 0), (768, 3072, 6368, True, True, 0), (2304, 768, 6368, True, True, 0),
+    (512, 2048, 2926, True, True, 0), (64, 72, 100, True, True, 3), (136, 200, 1, True, True, 2),
+    # dX = dY . W with W [out][in] read K-major
+    (6368, 768, 3072, False, True, 0), (2926, 2048, 512, False, True, 1), (100, 64, 192, False, True, 3),
+    (300, 200, 128, False, True, 2),
+    # A K-major, B row-major
+    (256, 128, 128, True, False, 1), (72, 64, 64, True, False, 3),
+])
+def test_gemm_kmajor(dev, M, N, K, ak, bk, tile):
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
+    A = torch.randn(K, M, generator=g).half().to(dev) if ak else torch.randn(M, K, generator=g).half().to(dev)
+    B = ((torch.randn(K, N, generator=g) if bk else torch.randn(N, K, generator=g)) * K ** -0.5).half().to(dev)
+    Ad = A.double().t() if ak else A.double()
+    Bd = B.double() if bk else B.double().t()
+    ref = Ad @ Bd
+    C = ops.gemm(A, B, epilogue=ops.EPI_NONE, tile=tile, a_kmajor=ak, b_kmajor=bk)
+    assert_ulps(C, ref, 1.0, 2e-2, f"gemm kmajor {ak}{bk}")
+    C32 = ops.gemm(A, B, epilogue=ops.EPI_F32, tile=tile, a_kmajor=ak, b_kmajor=bk)
+    torch.testing.assert_close(C32.double(), ref, rtol=1e-5, atol=1e-4)
+    # the NT form of the same product (explicit transposes) gives the identical fp32 accumulation order
+    if K % 64 == 0:
+        At = A.t().contiguous() if ak else A
+        Bt = B.t().contiguous() if bk else B
+        C0 = ops.gemm_nt(At, Bt, epilogue=ops.EPI_F32, tile=tile if tile in (1, 2, 3) else 1)
+        assert torch.equal(C0, C32)
+
+
+def test_gemm_kmajor_dgelu(dev):
+    torch.manual_seed(5)
+    M, N, K = 600, 1024, 256
+    dY = torch.randn(M, K).half().to(dev)
+    W = (torch.randn(K, N) * K ** -0.5).half().to(dev)   # nn.Linear weight [out=K][in=N]
+    F = torch.randn(M, N).half().to(dev)
+    a = ops.gemm(dY, W, aux_in=F, epilogue=ops.EPI_DGELU, b_kmajor=True)
+    b = ops.gemm_nt(dY, W.t().contiguous(), aux_in=F, epilogue=ops.EPI_DGELU, tile=1)
+    assert torch.equal(a, b)
+
+
 def _gelu16(f):
     t1 = (f.float() * 1.702).half()
     t2 = torch.sigmoid(t1.float()).half()
