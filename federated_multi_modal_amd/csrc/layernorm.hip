@@ -7,6 +7,8 @@
 // index gathers rows (ln_post on each image's class token, ln_final on each prompt's EOT token,
 // clip/model.py:567 and trainers/maple.py:72-76).  dgamma/dbeta are reduced deterministically:
 // per-block partial sums, then a column reduction (no float atomics).
+#include <cstdlib>
+
 #include "mf_common.h"
 
 #pragma clang fp contract(off)
@@ -168,14 +170,212 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const f16* __restrict__ dy,
   }
 }
 
+// ---- half-wave-per-row variants: 32 lanes own a row, 16-byte (8 x fp16) accesses, statistics by
+// 32-lane butterflies.  The forward puts 8 rows in flight per 256-thread block; the backward gives
+// every half-wave two rows whose loads are all issued before either is reduced.
+MF_DEV float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void ln_fwd2_kernel(const f16* __restrict__ x, int64_t ldx,
+                                                     const int* __restrict__ ridx, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, f16* __restrict__ y,
+                                                     int64_t ldy, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out, int rows) {
+  constexpr int CH = D / 256;  // 16-byte chunks per lane
+  const int hl = threadIdx.x & 31;
+  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (row >= rows) return;  // whole half-waves leave together: the butterflies stay within a half
+  const int src = ridx ? ridx[row] : row;
+  const f16* xr = x + (int64_t)src * ldx;
+  float v[CH * 8];
+  f16x8 t[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) t[j] = *(const f16x8*)(xr + 8 * (hl + 32 * j));
+  // Reduction order identical to ln_fwd_kernel's: a 16-byte chunk holds the 4-element groups of two
+  // of its lanes (2*hl and 2*hl+1); keep them as two partials, butterfly each over the half-wave
+  // (= that kernel's xor 32..2 steps) and add them last (= its xor-1 step).
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int j = 0; j < CH; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[j * 8 + e] = (float)t[j][e];
+      if (e < 4) s0 += v[j * 8 + e];
+      else s1 += v[j * 8 + e];
+    }
+  const float mean = (half_sum(s0) + half_sum(s1)) / (float)D;
+  float ss0 = 0.f, ss1 = 0.f;
+#pragma unroll
+  for (int j = 0; j < CH; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[j * 8 + e] - mean;
+      if (e < 4) ss0 += d * d;
+      else ss1 += d * d;
+    }
+  const float var = (half_sum(ss0) + half_sum(ss1)) / (float)D;
+  const float rstd = 1.0f / sqrtf(fmaxf(var, 0.f) + 1e-5f);
+  const float bias = -rstd * mean;
+  f16* yr = y + (int64_t)row * ldy;
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const int c = 8 * (hl + 32 * j);
+    const f32x4 g0 = *(const f32x4*)(gamma + c), g1 = *(const f32x4*)(gamma + c + 4);
+    const f32x4 b0 = *(const f32x4*)(beta + c), b1 = *(const f32x4*)(beta + c + 4);
+    f16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float tt = v[j * 8 + e] * rstd;
+      tt = tt + bias;
+      tt = tt * (e < 4 ? g0[e] : g1[e - 4]);
+      tt = tt + (e < 4 ? b0[e] : b1[e - 4]);
+      o[e] = (f16)tt;
+    }
+    *(f16x8*)(yr + c) = o;
+  }
+  if (hl == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void ln_bwd2_kernel(const f16* __restrict__ dy, int64_t lddy,
+                                                     const f16* __restrict__ x, int64_t ldx,
+                                                     const int* __restrict__ ridx, const float* __restrict__ gamma,
+                                                     const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, const f16* dres,
+                                                     int64_t ldres, f16* dx, int64_t lddx,
+                                                     float* __restrict__ dg_part, float* __restrict__ db_part,
+                                                     int rows) {
+  constexpr int CH = D / 256;
+  constexpr int RPH = LN_ROWS_PER_BLOCK / 8;  // rows per half-wave
+  __shared__ float red_g[8][D];
+  __shared__ float red_b[8][D];
+  const int hl = threadIdx.x & 31;
+  const int hw = threadIdx.x >> 5;
+  float gv[CH * 8];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const f32x4 g0 = *(const f32x4*)(gamma + 8 * (hl + 32 * j)), g1 = *(const f32x4*)(gamma + 8 * (hl + 32 * j) + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      gv[j * 8 + e] = g0[e];
+      gv[j * 8 + 4 + e] = g1[e];
+    }
+  }
+  float accg[CH * 8], accb[CH * 8];
+#pragma unroll
+  for (int i = 0; i < CH * 8; ++i) accg[i] = accb[i] = 0.f;
+  // every load of the half-wave's rows first (rows past the end clamp to a valid row and are skipped)
+  const int r0 = blockIdx.x * LN_ROWS_PER_BLOCK + hw * RPH;
+  f16x8 tx[RPH][CH], td[RPH][CH], tr[RPH][CH];
+  int srcs[RPH];
+  float means[RPH], rstds[RPH];
+#pragma unroll
+  for (int k = 0; k < RPH; ++k) {
+    const int row = min(r0 + k, rows - 1);
+    srcs[k] = ridx ? ridx[row] : row;
+    means[k] = mean_in[row];
+    rstds[k] = rstd_in[row];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int c = 8 * (hl + 32 * j);
+      tx[k][j] = *(const f16x8*)(x + (int64_t)srcs[k] * ldx + c);
+      td[k][j] = *(const f16x8*)(dy + (int64_t)row * lddy + c);
+      if (dres) tr[k][j] = *(const f16x8*)(dres + (int64_t)srcs[k] * ldres + c);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < RPH; ++k) {
+    if (r0 + k < rows) {
+      const float mean = means[k], rstd = rstds[k];
+      float sdg0 = 0.f, sdg1 = 0.f, sdgx0 = 0.f, sdgx1 = 0.f;  // ln_bwd_kernel's order (see ln_fwd2_kernel)
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xv = (float)tx[k][j][e], dv = (float)td[k][j][e];
+          const float dg = dv * gv[j * 8 + e];
+          if (e < 4) {
+            sdg0 += dg;
+            sdgx0 += dg * xv;
+          } else {
+            sdg1 += dg;
+            sdgx1 += dg * xv;
+          }
+          const float xhat = (xv - mean) * rstd;
+          accg[j * 8 + e] += dv * xhat;
+          accb[j * 8 + e] += dv;
+        }
+      const float sdg = half_sum(sdg0) + half_sum(sdg1);
+      const float sdgx = half_sum(sdgx0) + half_sum(sdgx1);
+      const float invD = 1.0f / (float)D;
+      const float b = (sdg * mean - sdgx) * rstd * rstd * rstd * invD;
+      const float c = -b * mean - sdg * rstd * invD;
+      f16* dxr = dx + (int64_t)srcs[k] * lddx;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        f16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float t = ((rstd * (float)td[k][j][e]) * gv[j * 8 + e] + b * (float)tx[k][j][e]) + c;
+          const float t16 = r16(t);
+          o[e] = dres ? (f16)((float)tr[k][j][e] + t16) : (f16)t16;
+        }
+        *(f16x8*)(dxr + 8 * (hl + 32 * j)) = o;
+      }
+    }
+  }
+  // the 8 half-waves' column partials through LDS (fixed order: deterministic)
+#pragma unroll
+  for (int j = 0; j < CH; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red_g[hw][8 * (hl + 32 * j) + e] = accg[j * 8 + e];
+      red_b[hw][8 * (hl + 32 * j) + e] = accb[j * 8 + e];
+    }
+  __syncthreads();
+  for (int col = threadIdx.x; col < D; col += 256) {
+    float sg = 0.f, sb = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sg += red_g[k][col];
+      sb += red_b[k][col];
+    }
+    dg_part[(int64_t)blockIdx.x * D + col] = sg;
+    db_part[(int64_t)blockIdx.x * D + col] = sb;
+  }
+}
+
+// A/B knob: MAPFED_LN=1 selects the wave-per-row kernels
+inline int ln_variant() {
+  static const int v = getenv("MAPFED_LN") ? atoi(getenv("MAPFED_LN")) : 2;
+  return v;
+}
+
 }  // namespace
 
 extern "C" int mf_layernorm_fwd(const void* x, int64_t ldx, const int* row_index, const float* gamma,
                                 const float* beta, void* y, int64_t ldy, float* mean, float* rstd, int rows, int D,
                                 void* stream) {
   if (rows <= 0) return 0;
-  dim3 grid((rows + LN_WAVES - 1) / LN_WAVES);
   hipStream_t st = (hipStream_t)stream;
+  const bool v16 = ((uintptr_t)x % 16 == 0) && ((uintptr_t)y % 16 == 0) && (ldx % 8 == 0) && (ldy % 8 == 0);
+  if (ln_variant() == 2 && v16 && (D == 768 || D == 512)) {
+    const dim3 g2((rows + 7) / 8);
+    if (D == 768)
+      ln_fwd2_kernel<768><<<g2, 256, 0, st>>>((const f16*)x, ldx, row_index, gamma, beta, (f16*)y, ldy, mean, rstd, rows);
+    else
+      ln_fwd2_kernel<512><<<g2, 256, 0, st>>>((const f16*)x, ldx, row_index, gamma, beta, (f16*)y, ldy, mean, rstd, rows);
+    MF_CHECK_LAUNCH();
+    return 0;
+  }
+  dim3 grid((rows + LN_WAVES - 1) / LN_WAVES);
   if (D == 768)
     ln_fwd_kernel<768><<<grid, 256, 0, st>>>((const f16*)x, ldx, row_index, gamma, beta, (f16*)y, ldy, mean, rstd, rows);
   else if (D == 512)
@@ -198,7 +398,17 @@ extern "C" int mf_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int
   float* dg_part = workspace;
   float* db_part = workspace + (int64_t)nblk * D;
   hipStream_t st = (hipStream_t)stream;
-  if (D == 768)
+  const bool v16 = ((uintptr_t)dy % 16 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)dx % 16 == 0) &&
+                   (!dres || ((uintptr_t)dres % 16 == 0 && ldres % 8 == 0)) && lddy % 8 == 0 && ldx % 8 == 0 &&
+                   lddx % 8 == 0;
+  if (ln_variant() == 2 && v16) {
+    if (D == 768)
+      ln_bwd2_kernel<768><<<nblk, 256, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, row_index, gamma, mean, rstd,
+                                                (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows);
+    else
+      ln_bwd2_kernel<512><<<nblk, 256, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, row_index, gamma, mean, rstd,
+                                                (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows);
+  } else if (D == 768)
     ln_bwd_kernel<768><<<nblk, 256, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, row_index, gamma, mean, rstd,
                                              (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows);
   else
