@@ -253,6 +253,116 @@ __global__ void small_linear_bwd_dw_kernel(const T* __restrict__ dY, const T* __
   }
 }
 
+// ---------------------------------------------------------------- batched small linears
+// Every Linear of the prompt learner (proj_lang_to_vis on ctx, the J-1 compound prompt projections)
+// in ONE launch per direction, driven by a device descriptor table: they are independent of each
+// other in both directions (distinct outputs, distinct gradient targets), and each is far too small
+// to fill the chip alone (<= 2 x 768 outputs), so their launch latencies were the cost.
+struct LinDesc {
+  const void* X;   // [M, I]
+  const void* W;   // [O, I]
+  const void* b;   // [O] or null
+  void* Y;         // [M, O]
+  const void* dY;  // [M, O]
+  void* dX;        // [M, I] or null (accumulated when acc_dx)
+  void* dW;        // [O, I] or null
+  void* db;        // [O] or null
+  int M, I, O, is16, acc_dx, pad;
+};
+
+template <typename T>
+MF_DEV float ldv(const void* p, int64_t i) { return (float)((const T*)p)[i]; }
+
+// grid (ceil(maxMO / 4), n): wave w of block x computes output (m, o) = 4x + w of descriptor y
+__global__ __launch_bounds__(256) void lin_fwd_batch_kernel(const LinDesc* __restrict__ descs) {
+  const LinDesc d = descs[blockIdx.y];
+  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (idx >= d.M * d.O) return;
+  const int m = idx / d.O, o = idx % d.O;
+  float s = 0.f;
+  if (d.is16) {
+    for (int i = lane; i < d.I; i += 64) s += ldv<f16>(d.X, (int64_t)m * d.I + i) * ldv<f16>(d.W, (int64_t)o * d.I + i);
+  } else {
+    for (int i = lane; i < d.I; i += 64) s += ldv<float>(d.X, (int64_t)m * d.I + i) * ldv<float>(d.W, (int64_t)o * d.I + i);
+  }
+  s = wave_sum(s);
+  if (lane == 0) {
+    if (d.is16)
+      ((f16*)d.Y)[(int64_t)m * d.O + o] = (f16)(s + (d.b ? ldv<f16>(d.b, o) : 0.f));
+    else
+      ((float*)d.Y)[(int64_t)m * d.O + o] = s + (d.b ? ldv<float>(d.b, o) : 0.f);
+  }
+}
+
+// dX[m,i] (=|+=) sum_o dY[m,o] W[o,i]: grid (ceil(maxI/64), maxM, n), 1024 threads, 16 wave groups
+// split the o range (fixed-order LDS reduction: deterministic), as small_linear_bwd_dx_kernel
+__global__ __launch_bounds__(1024) void lin_bwd_dx_batch_kernel(const LinDesc* __restrict__ descs) {
+  __shared__ float red[16][65];
+  const LinDesc d = descs[blockIdx.z];
+  if (!d.dX || (int)blockIdx.y >= d.M || (int)blockIdx.x * 64 >= d.I) return;
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane, m = blockIdx.y;
+  float s0 = 0.f, s1 = 0.f;
+  if (i < d.I) {
+    int o = g;
+    if (d.is16) {
+      for (; o + 16 < d.O; o += 32) {
+        s0 += ldv<f16>(d.dY, (int64_t)m * d.O + o) * ldv<f16>(d.W, (int64_t)o * d.I + i);
+        s1 += ldv<f16>(d.dY, (int64_t)m * d.O + o + 16) * ldv<f16>(d.W, (int64_t)(o + 16) * d.I + i);
+      }
+      for (; o < d.O; o += 16) s0 += ldv<f16>(d.dY, (int64_t)m * d.O + o) * ldv<f16>(d.W, (int64_t)o * d.I + i);
+    } else {
+      for (; o + 16 < d.O; o += 32) {
+        s0 += ldv<float>(d.dY, (int64_t)m * d.O + o) * ldv<float>(d.W, (int64_t)o * d.I + i);
+        s1 += ldv<float>(d.dY, (int64_t)m * d.O + o + 16) * ldv<float>(d.W, (int64_t)(o + 16) * d.I + i);
+      }
+      for (; o < d.O; o += 16) s0 += ldv<float>(d.dY, (int64_t)m * d.O + o) * ldv<float>(d.W, (int64_t)o * d.I + i);
+    }
+  }
+  red[g][lane] = s0 + s1;
+  __syncthreads();
+  if (g == 0 && i < d.I) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][lane];
+    const int64_t t = (int64_t)m * d.I + i;
+    if (d.is16) {
+      f16* dx = (f16*)d.dX;
+      dx[t] = d.acc_dx ? (f16)((float)dx[t] + (float)(f16)s) : (f16)s;
+    } else {
+      float* dx = (float*)d.dX;
+      dx[t] = d.acc_dx ? dx[t] + s : s;
+    }
+  }
+}
+
+// dW[o,i] = sum_m dY[m,o] X[m,i];  db[o] = sum_m dY[m,o]:  grid (ceil(maxOI/256), n)
+__global__ __launch_bounds__(256) void lin_bwd_dw_batch_kernel(const LinDesc* __restrict__ descs) {
+  const LinDesc d = descs[blockIdx.y];
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (!d.dW || t >= d.O * d.I) return;
+  const int o = t / d.I, i = t % d.I;
+  float s = 0.f, sb = 0.f;
+  if (d.is16) {
+    for (int m = 0; m < d.M; ++m) {
+      const float gy = ldv<f16>(d.dY, (int64_t)m * d.O + o);
+      s += gy * ldv<f16>(d.X, (int64_t)m * d.I + i);
+      sb += gy;
+    }
+    ((f16*)d.dW)[t] = (f16)s;
+    if (i == 0 && d.db) ((f16*)d.db)[o] = (f16)sb;
+  } else {
+    for (int m = 0; m < d.M; ++m) {
+      const float gy = ldv<float>(d.dY, (int64_t)m * d.O + o);
+      s += gy * ldv<float>(d.X, (int64_t)m * d.I + i);
+      sb += gy;
+    }
+    ((float*)d.dW)[t] = s;
+    if (i == 0 && d.db) ((float*)d.db)[o] = sb;
+  }
+}
+
 // ---------------------------------------------------------------- casts
 __global__ void cast_f16_to_f32_kernel(const f16* __restrict__ in, float* __restrict__ out, int64_t n) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -388,6 +498,25 @@ extern "C" int mf_small_linear_bwd(const void* dY, const void* X, const void* W,
 extern "C" int mf_cast_f16_f32(const void* in, float* out, int64_t n, void* stream) {
   if (n <= 0) return 0;
   cast_f16_to_f32_kernel<<<nblk(n), 256, 0, (hipStream_t)stream>>>((const f16*)in, out, n);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_small_linear_desc_bytes(void) { return (int)sizeof(LinDesc); }
+
+extern "C" int mf_small_linear_fwd_batch(const void* descs, int n, int max_mo, void* stream) {
+  if (n <= 0 || max_mo <= 0) return 0;
+  lin_fwd_batch_kernel<<<dim3((max_mo + 3) / 4, n), 256, 0, (hipStream_t)stream>>>((const LinDesc*)descs);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_small_linear_bwd_batch(const void* descs, int n, int max_m, int max_i, int max_oi, void* stream) {
+  if (n <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  lin_bwd_dx_batch_kernel<<<dim3((max_i + 63) / 64, max_m, n), 1024, 0, st>>>((const LinDesc*)descs);
+  MF_CHECK_LAUNCH();
+  lin_bwd_dw_batch_kernel<<<dim3((max_oi + 255) / 256, n), 256, 0, st>>>((const LinDesc*)descs);
   MF_CHECK_LAUNCH();
   return 0;
 }

@@ -433,6 +433,21 @@ class MapleEngine:
         self.dimg, self.dtxt = e(B, E), e(K, E)
         self.d_vis_post, self.d_txt_final = e(B, dv), e(K, dt)
         self.dXpre = e(B * self.Lv, dv)
+        # the prompt learner's Linears (proj_lang_to_vis on ctx + the J-1 compound projections), one
+        # launch per direction (trainers/maple.py:111-131, 194-215)
+        P, G = self.P, self.G
+        ents = [dict(X=P[pl + "ctx"], W=P[pl + "proj_lang_to_vis.weight"], b=P[pl + "proj_lang_to_vis.bias"],
+                     Y=self.shared_ctx, dY=self.g_shared_ctx, dX=G[pl + "ctx"], acc_dx=True,
+                     dW=G[pl + "proj_lang_to_vis.weight"], db=G[pl + "proj_lang_to_vis.bias"])]
+        for i in range(J - 1):
+            name = (pl + f"compound_prompts_text_parameters.{i // 2}" if i % 2 == 0
+                    else pl + f"visual_deep_prompts_parameters.{(i - 1) // 2}")
+            y, dy = (self.vis_deep[i], self.g_vis_deep[i]) if i % 2 == 0 else (self.txt_deep[i], self.g_txt_deep[i])
+            ents.append(dict(X=P[name], W=P[pl + f"compound_prompt_projections.{i}.weight"],
+                             b=P[pl + f"compound_prompt_projections.{i}.bias"], Y=y, dY=dy, dX=G[name], acc_dx=True,
+                             dW=G[pl + f"compound_prompt_projections.{i}.weight"],
+                             db=G[pl + f"compound_prompt_projections.{i}.bias"]))
+        self.pl_linears = ops.SmallLinearBatch(dev, ents)
 
 
     def load_batch(self, images: torch.Tensor, labels: Optional[torch.Tensor] = None):
@@ -443,38 +458,15 @@ class MapleEngine:
 
     # ------------------------------------------------------------------ prompt learner
     def _prompt_learner_fwd(self):
-        """MultiModalPromptLearner.forward (trainers/maple.py:177-218)."""
-        P = self.P
-        pl = "prompt_learner."
-        ops.small_linear_fwd(P[pl + "ctx"], P[pl + "proj_lang_to_vis.weight"], P[pl + "proj_lang_to_vis.bias"],
-                             self.shared_ctx)
-        for i in range(self.J - 1):
-            w = P[pl + f"compound_prompt_projections.{i}.weight"]
-            b = P[pl + f"compound_prompt_projections.{i}.bias"]
-            if i % 2 == 0:
-                t = P[pl + f"compound_prompts_text_parameters.{i // 2}"]
-                ops.small_linear_fwd(t, w, b, self.vis_deep[i])
-            else:
-                v = P[pl + f"visual_deep_prompts_parameters.{(i - 1) // 2}"]
-                ops.small_linear_fwd(v, w, b, self.txt_deep[i])
+        """MultiModalPromptLearner.forward (trainers/maple.py:177-218): shared_ctx = proj_lang_to_vis(ctx)
+        and the J-1 compound projections, in one batched launch."""
+        self.pl_linears.fwd()
 
     def _prompt_learner_bwd(self):
-        P, G = self.P, self.G
-        pl = "prompt_learner."
-        for i in range(self.J - 1):
-            w = P[pl + f"compound_prompt_projections.{i}.weight"]
-            dw = G[pl + f"compound_prompt_projections.{i}.weight"]
-            db = G[pl + f"compound_prompt_projections.{i}.bias"]
-            if i % 2 == 0:
-                name = pl + f"compound_prompts_text_parameters.{i // 2}"
-                # G[name] already holds the text tower's gradient of the direct use (g_txt_deep[i])
-                ops.small_linear_bwd(self.g_vis_deep[i], P[name], w, G[name], dw, db, accumulate_dx=True)
-            else:
-                name = pl + f"visual_deep_prompts_parameters.{(i - 1) // 2}"
-                ops.small_linear_bwd(self.g_txt_deep[i], P[name], w, G[name], dw, db, accumulate_dx=True)
-        # ctx: text-path grad (already in G[ctx]) + fp16(d shared_ctx . W)
-        ops.small_linear_bwd(self.g_shared_ctx, P[pl + "ctx"], P[pl + "proj_lang_to_vis.weight"], G[pl + "ctx"],
-                             G[pl + "proj_lang_to_vis.weight"], G[pl + "proj_lang_to_vis.bias"], accumulate_dx=True)
+        """Their backward in one dX launch + one dW/db launch.  Each parameter's gradient already holds
+        the tower's gradient of its direct use (text ctx / deep prompts); the projection path adds to
+        it, as autograd accumulates the two uses (fp16 ctx: the new term rounded once, then added)."""
+        self.pl_linears.bwd()
 
     # ------------------------------------------------------------------ forward
     def _text_forward(self):

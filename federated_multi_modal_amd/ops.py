@@ -259,6 +259,38 @@ def small_linear_fwd(X, W, b, Y):
     return Y
 
 
+class SmallLinearBatch:
+    """A fixed set of small Linears (the prompt learner's) run as one launch per direction.  Each entry:
+    X [M,I], W [O,I], b [O] or None, Y [M,O]; backward: dY [M,O], dX (accumulated when acc_dx), dW, db.
+    The descriptor table is built once (static pointers, hipGraph-capturable)."""
+
+    def __init__(self, device, entries):
+        import numpy as np
+        assert call("mf_small_linear_desc_bytes") == 88
+        dt = np.dtype([("X", np.uint64), ("W", np.uint64), ("b", np.uint64), ("Y", np.uint64), ("dY", np.uint64),
+                       ("dX", np.uint64), ("dW", np.uint64), ("db", np.uint64), ("M", np.int32), ("I", np.int32),
+                       ("O", np.int32), ("is16", np.int32), ("acc", np.int32), ("pad", np.int32)])
+        arr = np.zeros(len(entries), dtype=dt)
+        ptr = lambda t: 0 if t is None else t.data_ptr()
+        self.max_mo = self.max_m = self.max_i = self.max_oi = 0
+        for k, e in enumerate(entries):
+            M, I = e["X"].shape
+            O = e["W"].shape[0]
+            arr[k] = (ptr(e["X"]), ptr(e["W"]), ptr(e.get("b")), ptr(e["Y"]), ptr(e.get("dY")), ptr(e.get("dX")),
+                      ptr(e.get("dW")), ptr(e.get("db")), M, I, O, int(e["X"].dtype == torch.float16),
+                      int(e.get("acc_dx", False)), 0)
+            self.max_mo, self.max_m = max(self.max_mo, M * O), max(self.max_m, M)
+            self.max_i, self.max_oi = max(self.max_i, I), max(self.max_oi, O * I)
+        self.n = len(entries)
+        self.descs = torch.from_numpy(arr.view(np.uint8)).to(device)
+
+    def fwd(self):
+        call("mf_small_linear_fwd_batch", _p(self.descs), self.n, self.max_mo, _s())
+
+    def bwd(self):
+        call("mf_small_linear_bwd_batch", _p(self.descs), self.n, self.max_m, self.max_i, self.max_oi, _s())
+
+
 def small_linear_bwd(dY, X, W, dX=None, dW=None, db=None, accumulate_dx=False):
     M, I = X.shape
     O = W.shape[0]

@@ -101,6 +101,14 @@ int mf_small_linear_fwd(const void* X, const void* W, const void* b, void* Y, in
 int mf_small_linear_bwd(const void* dY, const void* X, const void* W, void* dX, void* dW, void* db, int M, int I,
                         int O, int is_f16, int accumulate_dx, void* stream);
 
+/* Batched form: every Linear of the prompt learner in one launch per direction.  descs: device array
+ * of n descriptors of mf_small_linear_desc_bytes() bytes {const void *X, *W, *b; void *Y; const void* dY;
+ * void *dX, *dW, *db; int M, I, O, is_f16, accumulate_dx, pad} (b / dX / dW / db may be null);
+ * max_* bound the grid over the descriptors (M*O, M, I, O*I).                                         */
+int mf_small_linear_desc_bytes(void);
+int mf_small_linear_fwd_batch(const void* descs, int n, int max_mo, void* stream);
+int mf_small_linear_bwd_batch(const void* descs, int n, int max_m, int max_i, int max_oi, void* stream);
+
 /* ---- cosine-logit head + loss (trainers/maple.py:325,340-378) -------------------------------- */
 int mf_clip_head_fwd(const void* img, const void* txt, int B, int K, int D, const float* logit_scale, void* img_n,
                      void* txt_n, float* norms, void* mm, void* logits, void* stream);
