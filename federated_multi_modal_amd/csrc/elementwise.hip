@@ -143,11 +143,33 @@ __global__ __launch_bounds__(1024) void inject_bwd_kernel(f16* __restrict__ dx, 
 }
 
 // ---------------------------------------------------------------- transpose [R,C] -> [C,R]
-__global__ void transpose_kernel(const f16* __restrict__ in, int64_t ld_in, f16* __restrict__ out, int64_t ld_out,
-                                 int R, int C) {
-  __shared__ f16 tile[64][65];
+// 64 x 64 tiles, 256 threads: 16-byte loads (8 fp16 of a row) into a padded LDS tile, 16-byte stores
+// (8 fp16 of an output row = 8 input rows of one column).  Ragged edges fall back to element access.
+__global__ __launch_bounds__(256) void transpose_kernel(const f16* __restrict__ in, int64_t ld_in,
+                                                       f16* __restrict__ out, int64_t ld_out, int R, int C) {
+  __shared__ f16 tile[64][72];
   const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: 64 x 4
+  const int t = threadIdx.x;
+  const bool full = r0 + 64 <= R && c0 + 64 <= C && (ld_in % 8) == 0 && (ld_out % 8) == 0 &&
+                    ((uintptr_t)in % 16) == 0 && ((uintptr_t)out % 16) == 0;
+  if (full) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int r = t / 8 + 32 * k, c8 = (t % 8) * 8;
+      *(f16x8*)&tile[r][c8] = *(const f16x8*)(in + (int64_t)(r0 + r) * ld_in + c0 + c8);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = t / 8 + 32 * k, r8 = (t % 8) * 8;
+      f16x8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = tile[r8 + e][c];
+      *(f16x8*)(out + (int64_t)(c0 + c) * ld_out + r0 + r8) = v;
+    }
+    return;
+  }
+  const int tx = t & 63, ty = t >> 6;
   for (int i = ty; i < 64; i += 4) {
     const int r = r0 + i, c = c0 + tx;
     tile[i][tx] = (r < R && c < C) ? in[(int64_t)r * ld_in + c] : (f16)0.f;

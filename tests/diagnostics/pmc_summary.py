@@ -11,7 +11,7 @@ import json
 import sys
 from collections import defaultdict
 
-FAMILIES = [("gemm", "gemm_nt_kernel"), ("attention", "attn_"), ("layernorm", "ln_"), ("transpose", "transpose"),
+FAMILIES = [("gemm", "gemm"), ("attention", "attn_"), ("layernorm", "ln_"), ("transpose", "transpose"),
             ("optim", "sgd_kernel")]
 
 

@@ -264,6 +264,9 @@ def test_assemble_inject_transpose_colsum(dev):
     t = torch.zeros(200, 320, dtype=torch.float16, device=dev)
     ops.transpose(a, t[:, :300])
     assert torch.equal(t[:, :300], a.t()) and t[:, 300:].abs().max().item() == 0
+    for shape in ((3072, 768), (768, 2304), (130, 64)):  # 16-byte tile path + ragged fallback tiles
+        w = torch.randn(*shape).half().to(dev)
+        assert torch.equal(ops.transpose(w, torch.empty(shape[1], shape[0], dtype=torch.float16, device=dev)), w.t())
     cs = torch.empty(200, dtype=torch.float16, device=dev)
     ops.colsum(a, cs)
     assert (cs.float() - a.float().sum(0).half().float()).abs().max().item() <= ulp16(cs).max().item()
