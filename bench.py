@@ -17,6 +17,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import sys
 import time
 from pathlib import Path
@@ -182,12 +183,32 @@ def main():
     eng.overlap_towers = True
     ps = probe.summary()
 
+    # HBM traffic of the dominant kernel family, per launch, from the rocprofv3 PMC passes of this same
+    # command (scripts/gpu_pmc.sh -> profiles/*_<config>_pmc_summary.json: FETCH_SIZE doubled per
+    # MI355X_MICROARCH.md §HBM + WRITE_SIZE, memory-side counters); None when no summary exists
+    traffic = None
+    traffic_src = None
+    def _ver(path):  # r<round>_v<n>_... -> (round, n)
+        m = re.match(r"r(\d+)_v(\d+)_", path.name)
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+
+    pmc = sorted((ROOT / "profiles").glob(f"*_{args.config}_pmc_summary.json"), key=_ver)
+    if pmc and args.roofline_kernel == "gemm":
+        try:
+            fam = json.loads(pmc[-1].read_text()).get("gemm", {})
+            traffic = fam.get("hbm_bytes_per_launch")
+            traffic_src = str(pmc[-1].relative_to(ROOT))
+        except (OSError, ValueError):
+            traffic = None
+
     step_flop = B * FLOP_PER_IMAGE + K * FLOP_PER_CLASS
     value = world * B * args.steps / elapsed
     if args.roofline_kernel == "gemm":
         roof = {"bound": "mfma", "achieved": ps["tflops"], "peak": MFMA_PEAK_F16 / 1e12, "unit": "TFLOP/s",
-                "frac": ps["tflops"] * 1e12 / MFMA_PEAK_F16, "traffic": None,
-                "kernel": "gemm_nt_kernel (all projection GEMMs, fwd+bwd)", "launches_per_step": ps["launches"] // 2,
+                "frac": ps["tflops"] * 1e12 / MFMA_PEAK_F16, "traffic": traffic, "traffic_unit": "bytes/launch",
+                "traffic_source": traffic_src, "algorithmic_bytes_per_launch": ps["bytes_per_launch"],
+                "kernel": "GEMM family: gemm_nt_kernel + gemm8_kernel (every projection GEMM, fwd+bwd)",
+                "launches_per_step": ps["launches"] // 2,
                 "avg_launch_us": ps["avg_us"], "flop_per_launch": ps["flops_per_launch"]}
     else:
         roof = {"bound": "mfma", "achieved": ps["tflops"], "peak": MFMA_PEAK_F16 / 1e12, "unit": "TFLOP/s",
