@@ -26,12 +26,30 @@ int main(int argc, char** argv) {
   unsigned long long* st;
   hipMalloc(&st, (size_t)NH * 64);
   hipMemcpyToSymbol(HIP_SYMBOL(g_astamps), &st, sizeof(st));
+  const bool fwd = getenv("STAMP_FWD") != nullptr;  // time the forward (attn_fwd_kernel) instead
   mf_attention_fwd(qkv, 3 * D, o, D, lse, L, N, L, H, causal, 0);
-  for (int rep = 0; rep < 5; ++rep) {
+  for (int rep = 0; rep < 5 && fwd; ++rep) {
+    hipMemset(st, 0, (size_t)NH * 64);
+    mf_attention_fwd(qkv, 3 * D, o, D, lse, L, N, L, H, causal, 0);
+    hipDeviceSynchronize();
+  }
+  for (int rep = 0; rep < 5 && !fwd; ++rep) {
     hipMemset(st, 0, (size_t)NH * 64);
     int rc = mf_attention_bwd(qkv, 3 * D, o, D, dout, D, lse, ws, L, dqkv, 3 * D, N, L, H, causal, 0);
     if (rc) { printf("error %s\n", mf_last_error()); return 1; }
     hipDeviceSynchronize();
+  }
+  if (fwd) {  // attn_fwd_kernel: grid (N*H, qsplit); only blockIdx.y == 0 records (its block id = x)
+    std::vector<unsigned long long> s((size_t)NH * 8);
+    hipMemcpy(s.data(), st, s.size() * 8, hipMemcpyDeviceToHost);
+    const char* fn[3] = {"stage", "pass1(max)", "pass2(PV)"};
+    for (int k = 0; k < 3; ++k) {
+      std::vector<double> v;
+      for (int b = 0; b < NH; ++b) if (s[b * 8 + k + 1] && s[b * 8 + k]) v.push_back((s[b * 8 + k + 1] - s[b * 8 + k]) / 100.0);
+      std::sort(v.begin(), v.end());
+      if (!v.empty()) printf("  fwd %-10s min %7.2f  med %7.2f  p90 %7.2f  max %7.2f us\n", fn[k], v[0], v[v.size() / 2], v[v.size() * 9 / 10], v.back());
+    }
+    return 0;
   }
   std::vector<unsigned long long> s((size_t)NH * 8);
   hipMemcpy(s.data(), st, s.size() * 8, hipMemcpyDeviceToHost);
