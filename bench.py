@@ -173,15 +173,27 @@ def main():
     # ---------------- per-launch roofline of the dominant kernel (eager pass, HIP events on the
     # launching stream around every launch of that kernel during 2 full steps)
     # (towers serialised on one stream here so that no other kernel runs inside a probed launch)
-    probe = ops.KernelProbe(args.roofline_kernel)
+    probe = ops.KernelProbe({"gemm": "gemm", "attention_fwd": "attention"}[args.roofline_kernel])
+    aprobe = ops.KernelProbe("attention") if args.roofline_kernel == "gemm" else probe
     eng.overlap_towers = False
-    ops.set_probe(probe)
-    for i in range(2):
-        load(i)
-        eng.train_step()
-    ops.set_probe(None)
+    for pr in dict.fromkeys((probe, aprobe)):  # the GEMM probe, then the attention probe (own steps)
+        ops.set_probe(pr)
+        for i in range(2):
+            load(i)
+            eng.train_step()
+        ops.set_probe(None)
     eng.overlap_towers = True
-    ps = probe.summary()
+    ps = probe.summary("gemm" if args.roofline_kernel == "gemm" else "attention_fwd")
+    # the attention kernels (north star: their MFMA-roofline fraction) against both roofs, per direction and
+    # tower; at these lengths they sit below the 312 flop/B ridge, so the HBM roof binds
+    attn_roof = {}
+    for key in aprobe.keys():
+        a = aprobe.summary(key)
+        attn_roof[key] = {"launches_per_step": a["launches"] // 2, "avg_launch_us": a["avg_us"],
+                          "flop_per_launch": a["flops_per_launch"], "bytes_per_launch": a["bytes_per_launch"],
+                          "tflops": a["tflops"], "mfma_frac": a["tflops"] * 1e12 / MFMA_PEAK_F16,
+                          "gbs": a["gbs"], "hbm_frac": a["gbs"] * 1e9 / HBM_PEAK,
+                          "flop_per_byte": a["flops_per_launch"] / max(a["bytes_per_launch"], 1.0)}
 
     # HBM traffic of the dominant kernel family, per launch, from the rocprofv3 PMC passes of this same
     # command (scripts/gpu_pmc.sh -> profiles/*_<config>_pmc_summary.json: FETCH_SIZE doubled per
@@ -238,6 +250,7 @@ def main():
         "model_mfma_frac": world * step_flop * args.steps / elapsed / MFMA_PEAK_F16 / world,
         "loss": loss,
         "roofline": roof,
+        "attention_roofline": attn_roof,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

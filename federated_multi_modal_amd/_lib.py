@@ -41,6 +41,7 @@ SIGNATURES = {
     "mf_small_linear_bwd_batch": [P, I, I, I, I, P],
     "mf_clip_head_fwd": [P, P, I, I, I, P, P, P, P, P, P, P],
     "mf_clip_loss_fwd_bwd": [P, P, P, P, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P],
+    "mf_clip_loss_soft_fwd_bwd": [P, P, P, P, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P],
     "mf_argmax_correct": [P, I, I, P, P, P, P],
     "mf_optim_chunk_bytes": [],
     "mf_optim_chunk_elems": [],

@@ -2,6 +2,8 @@
 //   img_n = F.normalize(img, eps=1e-8), txt_n = F.normalize(txt, eps=1e-8)  (fp16: x / fp16(||x||))
 //   logits = fp16(min(exp(logit_scale),100) * fp16(img_n @ txt_n^T))
 //   loss   = CE(logits, y) + 0.5 * (1 - mean_b cos(img_n[b], txt_n[y_b]))
+// or, for soft (float) labels q [B,K] (trainers/maple.py:356-360),
+//   loss   = KL(q.clamp(1e-8) || softmax) (batchmean, fp32) + 0.5 * (1 - mean_b cos(img_n[b], (q @ txt_n)[b]))
 // and the analytic backward to d img / d txt (fp32 math, fp16 outputs at the tensor boundaries
 // the reference materialises).  Small: B <= 64 rows, K <= 1000 classes, width 512.
 #include "mf_common.h"
@@ -115,18 +117,19 @@ __global__ void loss_kernel(const f16* __restrict__ logits, const f16* __restric
 
 // d img_n[b,:] = fp16( fp16(sum_k dmm[b,k] txt_n[k,:]) + cos-path ) ; block per row b
 // cos path (fp32): g_u = dcos*v, d img_n += g_u/nu - img_n*(g_u . img_n)/nu^3 with dcos = fp16(-0.5/B)
+// soft_rows != null: the cosine target of row b is soft_rows[b,:] ((q @ txt_n)[b]) instead of txt_n[y_b]
 __global__ void dimg_kernel(const f16* __restrict__ dmm, const f16* __restrict__ img_n, const f16* __restrict__ txt_n,
-                            const int64_t* __restrict__ label, const float* __restrict__ cos_norms, int B, int K,
-                            int D, f16* __restrict__ dimg_n) {
+                            const int64_t* __restrict__ label, const f16* __restrict__ soft_rows,
+                            const float* __restrict__ cos_norms, int B, int K, int D, f16* __restrict__ dimg_n) {
   const int b = blockIdx.x;
-  const int y = (int)label[b];
+  const f16* trow = soft_rows ? soft_rows + (int64_t)b * D : txt_n + (int64_t)label[b] * D;
   const float dcos = r16(-0.5f / (float)B);
   const float nu = cos_norms[2 * b], nv = cos_norms[2 * b + 1];
   __shared__ float red[4];
   // g_u . img_n
   float dotp = 0.f;
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    float v = r16((float)txt_n[(int64_t)y * D + d] / nv);
+    float v = r16((float)trow[d] / nv);
     dotp += dcos * v * (float)img_n[(int64_t)b * D + d];
   }
   dotp = wave_sum(dotp);
@@ -136,7 +139,7 @@ __global__ void dimg_kernel(const f16* __restrict__ dmm, const f16* __restrict__
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
     float s = 0.f;
     for (int k = 0; k < K; ++k) s += (float)dmm[(int64_t)b * K + k] * (float)txt_n[(int64_t)k * D + d];
-    const float v = r16((float)txt_n[(int64_t)y * D + d] / nv);
+    const float v = r16((float)trow[d] / nv);
     const float a = (float)img_n[(int64_t)b * D + d];
     const float cosg = dcos * v / nu - a * dotp / (nu * nu * nu);
     dimg_n[(int64_t)b * D + d] = (f16)(r16(s) + r16(cosg));
@@ -179,6 +182,125 @@ __global__ void dtxt_kernel(const f16* __restrict__ dmm, const f16* __restrict__
       cg += dcos * u / nv - t * dots[b] / (nv * nv * nv);
     }
     dtxt_n[(int64_t)k * D + d] = (f16)(r16(s) + (cg != 0.f ? r16(cg) : 0.f));
+  }
+}
+
+
+// ---- soft labels (trainers/maple.py:356-360) -------------------------------------------------------
+// text_features_for_images = q @ txt_n: tgt[b,:] = fp16(sum_k fp16(q[b,k]) txt_n[k,:]), fp32 accumulate.
+// The reference multiplies an fp32 label by the fp16 text features, which torch refuses
+// ("expected m1 and m2 to have the same dtype") in its fp16 configuration; the label is taken in the
+// text features' dtype, which is also what the product computes under torch.autocast.  Block per b.
+__global__ void soft_target_kernel(const float* __restrict__ q, const f16* __restrict__ txt_n, int K, int D,
+                                   f16* __restrict__ tgt) {
+  const int b = blockIdx.x;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) s += r16(q[(int64_t)b * K + k]) * (float)txt_n[(int64_t)k * D + d];
+    tgt[(int64_t)b * D + d] = (f16)s;
+  }
+}
+
+// Single block of 256 threads, wave w handles rows b = w, w+4, ...
+//   log_probs = fp16(log_softmax(logits)); t = max(q, 1e-8)
+//   KL = sum_{b,k} t (log t - log_probs) / B  in fp32 (F.kl_div(..., "batchmean") of an fp16 input and an
+//   fp32 target promotes to fp32); its input gradient fp16(-t/B) goes through the log_softmax backward:
+//   dlogits = fp16(g - exp(log_probs) * sum_k g), dmm = fp16(dlogits * scale).
+//   cos_b = cos(img_n[b], tgt[b]) as loss_kernel; its gradient w.r.t. tgt[b] (fp16) is written to gtgt.
+// loss_out: [0] total = KL + fp16(0.5 * align) (fp32), [1] KL, [2] align, [3] nonfinite flag
+__global__ void loss_soft_kernel(const f16* __restrict__ logits, const f16* __restrict__ img_n,
+                                 const f16* __restrict__ tgt, const float* __restrict__ q, int B, int K, int D,
+                                 const float* __restrict__ logit_scale, f16* __restrict__ dmm,
+                                 f16* __restrict__ gtgt, float* __restrict__ cos_out, float* __restrict__ loss_out) {
+  __shared__ float s_kl[64], s_cos[64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const float sc = fminf(expf(logit_scale[0]), 100.f);
+  const float invB = 1.0f / (float)B;
+  const float dcos = r16(-0.5f * invB);
+  for (int b = w; b < B; b += 4) {
+    const f16* lr = logits + (int64_t)b * K;
+    const float* qr = q + (int64_t)b * K;
+    float mx = -INFINITY;
+    for (int k = lane; k < K; k += 64) mx = fmaxf(mx, (float)lr[k]);
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int k = lane; k < K; k += 64) se += expf((float)lr[k] - mx);
+    se = wave_sum(se);
+    const float lse = logf(se);
+    float kl = 0.f, sg = 0.f;
+    for (int k = lane; k < K; k += 64) {
+      const float logp = r16((float)lr[k] - mx - lse);
+      const float t = fmaxf(qr[k], 1e-8f);
+      kl += t * (logf(t) - logp);
+      sg += r16(-t * invB);
+    }
+    kl = wave_sum(kl);
+    sg = wave_sum(sg);
+    for (int k = lane; k < K; k += 64) {
+      const float logp = r16((float)lr[k] - mx - lse);
+      const float g = r16(-fmaxf(qr[k], 1e-8f) * invB);
+      const float dl = r16(g - expf(logp) * sg);
+      dmm[(int64_t)b * K + k] = (f16)(dl * sc);
+    }
+    const f16* tr = tgt + (int64_t)b * D;
+    const f16* ir = img_n + (int64_t)b * D;
+    float su = 0.f, sv = 0.f;
+    for (int d = lane; d < D; d += 64) {
+      const float a = (float)ir[d], t = (float)tr[d];
+      su += a * a;
+      sv += t * t;
+    }
+    const float nu = fmaxf(r16(sqrtf(wave_sum(su))), 1e-8f), nv = fmaxf(r16(sqrtf(wave_sum(sv))), 1e-8f);
+    float c = 0.f, dotp = 0.f;
+    for (int d = lane; d < D; d += 64) {
+      const float a = r16((float)ir[d] / nu), t = r16((float)tr[d] / nv);
+      c += r16(a * t);
+      dotp += dcos * a * (float)tr[d];
+    }
+    c = r16(wave_sum(c));
+    dotp = wave_sum(dotp);
+    // d tgt[b,:] = dcos * u / nv - tgt * (dcos u . tgt) / nv^3   (the txt side of dtxt_kernel's cos path)
+    for (int d = lane; d < D; d += 64) {
+      const float a = r16((float)ir[d] / nu);
+      gtgt[(int64_t)b * D + d] = (f16)(dcos * a / nv - (float)tr[d] * dotp / (nv * nv * nv));
+    }
+    if (lane == 0) {
+      s_kl[b] = kl;
+      s_cos[b] = c;
+      cos_out[2 * b] = nu;
+      cos_out[2 * b + 1] = nv;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float kl = 0.f, cs = 0.f;
+    for (int b = 0; b < B; ++b) {
+      kl += s_kl[b];
+      cs += s_cos[b];
+    }
+    kl = kl / (float)B;
+    const float align = r16(1.f - r16(cs / (float)B));
+    const float total = kl + r16(0.5f * align);
+    loss_out[0] = total;
+    loss_out[1] = kl;
+    loss_out[2] = align;
+    loss_out[3] = isfinite(total) ? 0.f : 1.f;
+  }
+}
+
+// d txt_n[k,:] = fp16( fp16(sum_b dmm[b,k] img_n[b,:]) + fp16(sum_b fp16(q[b,k]) gtgt[b,:]) ): the logits
+// product's gradient plus the q @ txt_n product's (q^T . d tgt); block per k
+__global__ void dtxt_soft_kernel(const f16* __restrict__ dmm, const f16* __restrict__ img_n,
+                                 const float* __restrict__ q, const f16* __restrict__ gtgt, int B, int K, int D,
+                                 f16* __restrict__ dtxt_n) {
+  const int k = blockIdx.x;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f, cg = 0.f;
+    for (int b = 0; b < B; ++b) {
+      s += (float)dmm[(int64_t)b * K + k] * (float)img_n[(int64_t)b * D + d];
+      cg += r16(q[(int64_t)b * K + k]) * (float)gtgt[(int64_t)b * D + d];
+    }
+    dtxt_n[(int64_t)k * D + d] = (f16)(r16(s) + r16(cg));
   }
 }
 
@@ -280,10 +402,33 @@ extern "C" int mf_clip_loss_fwd_bwd(const void* img, const void* txt, const void
   hipStream_t st = (hipStream_t)stream;
   loss_kernel<<<1, 256, 0, st>>>((const f16*)logits, (const f16*)img_n, (const f16*)txt_n, label, B, K, D,
                                  logit_scale, (f16*)dmm, cos_ws, loss_out);
-  dimg_kernel<<<B, 256, 0, st>>>((const f16*)dmm, (const f16*)img_n, (const f16*)txt_n, label, cos_ws, B, K, D,
-                                 (f16*)dimg_n);
+  dimg_kernel<<<B, 256, 0, st>>>((const f16*)dmm, (const f16*)img_n, (const f16*)txt_n, label, nullptr, cos_ws, B,
+                                 K, D, (f16*)dimg_n);
   dtxt_kernel<<<K, 256, 0, st>>>((const f16*)dmm, (const f16*)img_n, (const f16*)txt_n, label, cos_ws, B, K, D,
                                  (f16*)dtxt_n);
+  normalize_bwd_kernel<<<(B + 3) / 4, 256, 0, st>>>((const f16*)img, (const f16*)dimg_n, norms, (f16*)dimg, B, D);
+  normalize_bwd_kernel<<<(K + 3) / 4, 256, 0, st>>>((const f16*)txt, (const f16*)dtxt_n, norms + B, (f16*)dtxt, K, D);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+// soft_ws: 2*B*D fp16 (the targets q @ txt_n and their gradient)
+extern "C" int mf_clip_loss_soft_fwd_bwd(const void* img, const void* txt, const void* img_n, const void* txt_n,
+                                         const float* norms, const void* logits, const float* label_probs, int B,
+                                         int K, int D, const float* logit_scale, void* dmm, float* cos_ws,
+                                         void* soft_ws, float* loss_out, void* dimg_n, void* dtxt_n, void* dimg,
+                                         void* dtxt, void* stream) {
+  if (B > 64) return mf_set_error("mf_clip_loss_soft_fwd_bwd: B <= 64", -1);
+  hipStream_t st = (hipStream_t)stream;
+  f16* tgt = (f16*)soft_ws;
+  f16* gtgt = tgt + (int64_t)B * D;
+  soft_target_kernel<<<B, 256, 0, st>>>(label_probs, (const f16*)txt_n, K, D, tgt);
+  loss_soft_kernel<<<1, 256, 0, st>>>((const f16*)logits, (const f16*)img_n, tgt, label_probs, B, K, D, logit_scale,
+                                      (f16*)dmm, gtgt, cos_ws, loss_out);
+  dimg_kernel<<<B, 256, 0, st>>>((const f16*)dmm, (const f16*)img_n, (const f16*)txt_n, nullptr, tgt, cos_ws, B, K, D,
+                                 (f16*)dimg_n);
+  dtxt_soft_kernel<<<K, 256, 0, st>>>((const f16*)dmm, (const f16*)img_n, label_probs, gtgt, B, K, D,
+                                      (f16*)dtxt_n);
   normalize_bwd_kernel<<<(B + 3) / 4, 256, 0, st>>>((const f16*)img, (const f16*)dimg_n, norms, (f16*)dimg, B, D);
   normalize_bwd_kernel<<<(K + 3) / 4, 256, 0, st>>>((const f16*)txt, (const f16*)dtxt_n, norms + B, (f16*)dtxt, K, D);
   MF_CHECK_LAUNCH();

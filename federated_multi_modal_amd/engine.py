@@ -394,6 +394,9 @@ class MapleEngine:
         e = lambda *s, dt_=F16: torch.empty(*s, device=dev, dtype=dt_)
         self.img_in = e(B, 3, d.image_resolution, d.image_resolution, dt_=F32)
         self.label_in = torch.zeros(B, device=dev, dtype=torch.int64)
+        # soft (float) labels [B, K] select the KL branch of the loss (trainers/maple.py:356-360)
+        self.soft_label_in = torch.zeros(B, K, device=dev, dtype=F32)
+        self.soft_labels = False
         self.im2col = e(B * self.G2, 3 * d.vision_patch ** 2)
         self.patch = e(B * self.G2, dv)
         self.Xpre = e(B * self.Lv, dv)
@@ -428,6 +431,7 @@ class MapleEngine:
         self.norms = e(B + K, dt_=F32)
         self.mm, self.logits, self.dmm = e(B, K), e(B, K), e(B, K)
         self.cos_ws = e(2 * B, dt_=F32)
+        self.soft_ws = e(2 * B * E)
         self.loss_out = torch.zeros(4, device=dev, dtype=F32)
         self.dimg_n, self.dtxt_n = e(B, E), e(K, E)
         self.dimg, self.dtxt = e(B, E), e(K, E)
@@ -454,7 +458,23 @@ class MapleEngine:
         """Copy a batch into the static input buffers (H2D when given host tensors)."""
         self.img_in.copy_(images, non_blocking=True)
         if labels is not None:
+            self.set_labels(labels)
+
+    def set_labels(self, labels: torch.Tensor):
+        """Integer labels [B] -> cross-entropy; float labels [B, K] (soft targets) -> the KL-divergence
+        branch (trainers/maple.py:356-363: `label.dtype == torch.float`).  Switching branch changes the
+        launched kernels, so a captured step is per branch (trainers.MapleTrainer keeps one per branch)."""
+        if labels.is_floating_point():
+            if labels.dtype != F32:
+                raise TypeError(f"soft labels must be float32 (the reference tests label.dtype == torch.float), "
+                                f"got {labels.dtype}")
+            if tuple(labels.shape) != (self.B, self.K):
+                raise ValueError(f"soft labels of shape {tuple(labels.shape)}; expected ({self.B}, {self.K})")
+            self.soft_label_in.copy_(labels, non_blocking=True)
+            self.soft_labels = True
+        else:
             self.label_in.copy_(labels, non_blocking=True)
+            self.soft_labels = False
 
     # ------------------------------------------------------------------ prompt learner
     def _prompt_learner_fwd(self):
@@ -549,9 +569,14 @@ class MapleEngine:
     def forward_backward(self):
         """loss = CustomCLIP(image, label); loss.backward()  — grads land in gflat16/gflat32."""
         self.forward()
-        ops.clip_loss_fwd_bwd(self.img_feat, self.txt_feat, self.img_n, self.txt_n, self.norms, self.logits,
-                              self.label_in, self.P["logit_scale"], self.dmm, self.cos_ws, self.loss_out,
-                              self.dimg_n, self.dtxt_n, self.dimg, self.dtxt)
+        if self.soft_labels:
+            ops.clip_loss_soft_fwd_bwd(self.img_feat, self.txt_feat, self.img_n, self.txt_n, self.norms,
+                                       self.logits, self.soft_label_in, self.P["logit_scale"], self.dmm, self.cos_ws,
+                                       self.soft_ws, self.loss_out, self.dimg_n, self.dtxt_n, self.dimg, self.dtxt)
+        else:
+            ops.clip_loss_fwd_bwd(self.img_feat, self.txt_feat, self.img_n, self.txt_n, self.norms, self.logits,
+                                  self.label_in, self.P["logit_scale"], self.dmm, self.cos_ws, self.loss_out,
+                                  self.dimg_n, self.dtxt_n, self.dimg, self.dtxt)
         main = torch.cuda.current_stream(self.device)
         side = self.side if self.overlap_towers else main
         side.wait_stream(main)

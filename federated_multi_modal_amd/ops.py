@@ -17,27 +17,37 @@ EPI_NONE, EPI_BIAS, EPI_BIAS_RESID, EPI_BIAS_GELU, EPI_DGELU, EPI_F32, EPI_RESID
 
 
 class KernelProbe:
-    """Brackets every launch of one kernel family with HIP events on the launching stream (used by
-    bench.py for the per-launch roofline; off by default, never active during graph capture)."""
+    """Brackets every launch of the probed kernel families with HIP events on the launching stream
+    (used by bench.py for the per-launch rooflines; off by default, never active during graph
+    capture).  kinds: "gemm", "attention" (or one name / an iterable); each record carries a key
+    ("gemm", "attention_fwd/L199", ...) so the families and towers are summarised separately."""
 
-    def __init__(self, kind: str):
-        self.kind = kind
-        self.records = []  # (start_event, end_event, flops, bytes)
+    def __init__(self, kinds="gemm"):
+        self.kinds = {kinds} if isinstance(kinds, str) else set(kinds)
+        self.kind = next(iter(self.kinds)) if len(self.kinds) == 1 else None  # single-family callers
+        self.records = []  # (key, start_event, end_event, flops, bytes)
 
-    def around(self, flops: float, nbytes: float):
+    def wants(self, kind: str) -> bool:
+        return kind in self.kinds
+
+    def around(self, flops: float, nbytes: float, key: str = "gemm"):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
-        self.records.append((s, e, flops, nbytes))
+        self.records.append((key, s, e, flops, nbytes))
         return e
 
-    def summary(self):
+    def keys(self):
+        return sorted({r[0] for r in self.records})
+
+    def summary(self, prefix: Optional[str] = None):
         torch.cuda.synchronize()
-        ms = [s.elapsed_time(e) for s, e, _, _ in self.records]
+        recs = [r for r in self.records if prefix is None or r[0].startswith(prefix)]
+        ms = [s.elapsed_time(e) for _, s, e, _, _ in recs]
         n = len(ms)
         tot_ms = sum(ms)
-        flops = sum(r[2] for r in self.records)
-        nbytes = sum(r[3] for r in self.records)
+        flops = sum(r[3] for r in recs)
+        nbytes = sum(r[4] for r in recs)
         return {"launches": n, "avg_us": 1e3 * tot_ms / max(n, 1), "flops_per_launch": flops / max(n, 1),
                 "bytes_per_launch": nbytes / max(n, 1), "tflops": flops / (tot_ms * 1e-3) / 1e12 if n else 0.0,
                 "gbs": nbytes / (tot_ms * 1e-3) / 1e9 if n else 0.0}
@@ -74,8 +84,8 @@ def gemm_nt(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NON
     aux = aux_in if aux_in is not None else aux_out
     ld_aux = _ld(aux) if aux is not None else 0
     ev = None
-    if _PROBE is not None and _PROBE.kind == "gemm":
-        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N))
+    if _PROBE is not None and _PROBE.wants("gemm"):
+        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), "gemm")
     call("mf_gemm_nt", _p(A), _ld(A), _p(B), _ld(B), _p(C), _ld(C), M, N, K, _p(bias), _p(aux_in), _p(aux_out),
          ld_aux, epilogue, tile, _s())
     if ev is not None:
@@ -96,8 +106,8 @@ def gemm(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NONE, 
     aux = aux_in if aux_in is not None else aux_out
     ld_aux = _ld(aux) if aux is not None else 0
     ev = None
-    if _PROBE is not None and _PROBE.kind == "gemm":
-        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N))
+    if _PROBE is not None and _PROBE.wants("gemm"):
+        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), "gemm")
     call("mf_gemm", _p(A), _ld(A), int(a_kmajor), _p(B), _ld(B), int(b_kmajor), _p(C), _ld(C), M, N, K, _p(bias),
          _p(aux_in), _p(aux_out), ld_aux, epilogue, tile, _s())
     if ev is not None:
@@ -187,9 +197,11 @@ def attention_fwd(qkv, N, L, H, causal, out=None, lse=None, ld_lse=None):
     if lse is None:
         lse = torch.empty(N * H * ld_lse, device=qkv.device, dtype=torch.float32)
     ev = None
-    if _PROBE is not None and _PROBE.kind == "attention_fwd":
-        # algorithmic: QK^T + PV = 4 L^2 64 flop per (sequence, head); bytes: Q,K,V read + O write (fp16)
-        ev = _PROBE.around(4.0 * N * H * L * L * 64, 2.0 * 4 * N * L * H * 64)
+    if _PROBE is not None and _PROBE.wants("attention"):
+        # algorithmic: QK^T + PV = 4 * pairs * 64 flop per (sequence, head), pairs = L^2 (L(L+1)/2 under
+        # the causal mask); bytes: Q, K, V read + O written (fp16) + the LSE (fp32)
+        pairs = L * (L + 1) / 2 if causal else L * L
+        ev = _PROBE.around(4.0 * N * H * pairs * 64, N * H * L * (2.0 * 4 * 64 + 4), f"attention_fwd/L{L}")
     call("mf_attention_fwd", _p(qkv), _ld(qkv), _p(out), _ld(out), _p(lse), ld_lse, N, L, H, int(causal), _s())
     if ev is not None:
         ev.record()
@@ -203,8 +215,16 @@ def attention_bwd(qkv, out, dout, lse, N, L, H, causal, dqkv=None, ws=None, ld_l
         dqkv = torch.empty_like(qkv)
     if ws is None:
         ws = torch.empty(N * H * ld_lse, device=qkv.device, dtype=torch.float32)
+    ev = None
+    if _PROBE is not None and _PROBE.wants("attention"):
+        # algorithmic: dV = P^T dO, dP = dO V^T, dK = dS^T Q, dQ = dS K: 8 * pairs * 64 flop (the
+        # recompute of S is not counted); bytes: Q, K, V, O, dO + LSE read, dQ, dK, dV written
+        pairs = L * (L + 1) / 2 if causal else L * L
+        ev = _PROBE.around(8.0 * N * H * pairs * 64, N * H * L * (2.0 * 8 * 64 + 4), f"attention_bwd/L{L}")
     call("mf_attention_bwd", _p(qkv), _ld(qkv), _p(out), _ld(out), _p(dout), _ld(dout), _p(lse), _p(ws), ld_lse,
          _p(dqkv), _ld(dqkv), N, L, H, int(causal), _s())
+    if ev is not None:
+        ev.record()
     return dqkv
 
 
@@ -311,6 +331,22 @@ def clip_loss_fwd_bwd(img, txt, img_n, txt_n, norms, logits, label, logit_scale,
     K = txt.shape[0]
     call("mf_clip_loss_fwd_bwd", _p(img), _p(txt), _p(img_n), _p(txt_n), _p(norms), _p(logits), _p(label), B, K, D,
          _p(logit_scale), _p(dmm), _p(cos_ws), _p(loss_out), _p(dimg_n), _p(dtxt_n), _p(dimg), _p(dtxt), _s())
+
+
+
+def clip_loss_soft_fwd_bwd(img, txt, img_n, txt_n, norms, logits, label_probs, logit_scale, dmm, cos_ws, soft_ws,
+                           loss_out, dimg_n, dtxt_n, dimg, dtxt):
+    """Soft-label branch (trainers/maple.py:356-360): label_probs fp32 [B, K]; soft_ws fp16 >= 2*B*D."""
+    B, D = img.shape
+    K = txt.shape[0]
+    if label_probs.dtype != torch.float32 or tuple(label_probs.shape) != (B, K) or not label_probs.is_contiguous():
+        raise ValueError(f"soft labels must be contiguous fp32 [{B}, {K}], got {label_probs.dtype} "
+                         f"{tuple(label_probs.shape)}")
+    if soft_ws.dtype != torch.float16 or soft_ws.numel() < 2 * B * D:
+        raise ValueError("soft_ws: fp16 workspace of 2*B*D elements")
+    call("mf_clip_loss_soft_fwd_bwd", _p(img), _p(txt), _p(img_n), _p(txt_n), _p(norms), _p(logits),
+         _p(label_probs), B, K, D, _p(logit_scale), _p(dmm), _p(cos_ws), _p(soft_ws), _p(loss_out), _p(dimg_n),
+         _p(dtxt_n), _p(dimg), _p(dtxt), _s())
 
 
 def argmax_correct(logits, label=None, pred=None, acc=None):

@@ -192,7 +192,7 @@ class MaPLe(TrainerX):
         self.sched = self.optim.sched
         self.scaler = None
         self.register_model(f"MultiModalPromptLearner_{self.client_id}", self.model, self.optim, self.sched)
-        self._graph = None
+        self._graphs = {}
         self._loss_sum = torch.zeros(1, device=self.device)
         self._bad = torch.zeros(1, device=self.device)
         self._acc = torch.zeros(2, device=self.device)
@@ -216,10 +216,8 @@ class MaPLe(TrainerX):
         e = self.engine
         if image.shape[0] != e.B:
             raise ValueError(f"batch of {image.shape[0]} images; the client engine is built for {e.B}")
-        if label.is_floating_point():
-            raise NotImplementedError("soft (float) labels: the KL-divergence branch of trainers/maple.py:356-360")
         e.img_in.copy_(image, non_blocking=True)
-        e.label_in.copy_(label, non_blocking=True)
+        e.set_labels(label)  # float labels -> KL branch (trainers/maple.py:356-360)
 
     def _step_async(self, batch):
         """One forward_backward without host synchronisation; the loss accumulates on the device."""
@@ -228,11 +226,12 @@ class MaPLe(TrainerX):
         self._load(image, label)
         e = self.engine
         e.set_lr(self.optim.lr)
-        if self._graph is None:
-            e.train_step()          # first step eager: creates the momentum buffers
-            self._graph = e.capture_train_step()
+        g = self._graphs.get(e.soft_labels)  # one captured step per loss branch
+        if g is None:
+            e.train_step()          # first step of a branch eager (the first one creates the momentum buffers)
+            self._graphs[e.soft_labels] = e.capture_train_step()
         else:
-            self._graph.replay()
+            g.replay()
         self._loss_sum.add_(e.loss_out[0:1])
         self._bad.add_(e.loss_out[3:4])
 

@@ -116,6 +116,14 @@ int mf_clip_loss_fwd_bwd(const void* img, const void* txt, const void* img_n, co
                          const void* logits, const int64_t* label, int B, int K, int D, const float* logit_scale,
                          void* dmm, float* cos_ws, float* loss_out, void* dimg_n, void* dtxt_n, void* dimg,
                          void* dtxt, void* stream);
+/* Soft (float) labels q [B,K] fp32 (trainers/maple.py:356-360): KL(q.clamp(1e-8) || softmax) batchmean
+ * (fp32) + 0.5 (1 - mean cos(img_n, fp16(q) @ txt_n)); loss_out[0] is the fp32 total.  soft_ws: 2*B*D
+ * fp16 of workspace.  The reference's `label @ text_features` multiplies fp32 by fp16 and raises in its
+ * fp16 configuration; the label is taken in the features' dtype (what torch.autocast computes).       */
+int mf_clip_loss_soft_fwd_bwd(const void* img, const void* txt, const void* img_n, const void* txt_n,
+                              const float* norms, const void* logits, const float* label_probs, int B, int K, int D,
+                              const float* logit_scale, void* dmm, float* cos_ws, void* soft_ws, float* loss_out,
+                              void* dimg_n, void* dtxt_n, void* dimg, void* dtxt, void* stream);
 
 /* eval predictions (trainers/maple.py:674-677): pred[b] = argmax_k logits (first max; NaN is the max);
  * acc[0] += #correct, acc[1] += B (device-side accuracy counters, read once per test pass)           */

@@ -158,3 +158,38 @@ def test_training_is_deterministic_and_finite(dev):
         losses.append(ls)
     assert losses[0] == losses[1]
     assert all(np.isfinite(losses[0]))
+
+
+def test_engine_soft_labels_vs_oracle(dev):
+    """Soft (float) labels take the KL branch (trainers/maple.py:356-360): engine loss and gradients
+    against the oracle run in fp32 on the same inputs (B=4, K=10, depth 3), same tolerances as C1."""
+    from oracle import maple_oracle as O
+    J, K, B, seed = 3, 10, 4, 11
+    names = syn.synthetic_classnames(K, seed)
+    batch = syn.client_batch(seed, 0, 0, B, K)
+    g = torch.Generator().manual_seed(seed)
+    q = torch.rand(B, K, generator=g) ** 3
+    q[1] = torch.nn.functional.one_hot(torch.tensor(3), K).float()   # a hard row inside a soft batch
+    q = q / q.sum(1, keepdim=True)
+    e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed), device=dev)
+    e.load_batch(torch.from_numpy(batch.images), q)
+    assert e.soft_labels
+    e.forward_backward()
+    loss = e.loss()
+    grads = {k: v.detach().double().cpu().reshape(-1) for k, v in e.grads().items()}
+    M = O.build_model(seed, J, names, compute_dtype=torch.float32)
+    ref_loss, ref_grads, _ = O.train_step(M, torch.from_numpy(batch.images), q, O.SGDState(lr=0.0))
+    print(f"soft-label loss ours {loss:.5f} oracle(fp32) {ref_loss.item():.5f}")
+    assert abs(loss - ref_loss.item()) <= 5e-3
+    worst = []
+    for n, r in ref_grads.items():
+        r = r.double().reshape(-1)
+        if r.norm() == 0:
+            continue
+        worst.append(((grads[n] - r).norm().item() / r.norm().item(), n))
+    worst.sort(reverse=True)
+    print("worst soft-label grads (rel L2):", [(f"{a:.2e}", n) for a, n in worst[:5]])
+    assert worst[0][0] <= 5e-2, worst[0]
+    # switching back to integer labels returns to the cross-entropy branch
+    e.load_batch(torch.from_numpy(batch.images), torch.from_numpy(batch.labels))
+    assert not e.soft_labels

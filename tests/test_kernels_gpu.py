@@ -360,6 +360,75 @@ def test_clip_head_loss(dev):
     torch.testing.assert_close(dtxt.float(), t32.grad, rtol=2e-2, atol=2e-4)
 
 
+
+def _head_setup(dev, B, K, D, seed):
+    torch.manual_seed(seed)
+    img = torch.randn(B, D).half().to(dev)
+    txt = torch.randn(K, D).half().to(dev)
+    ls = torch.tensor([math.log(1 / 0.07)], device=dev)
+    img_n, txt_n = torch.empty_like(img), torch.empty_like(txt)
+    norms = torch.empty(B + K, device=dev)
+    mm = torch.empty(B, K, dtype=torch.float16, device=dev)
+    logits = torch.empty_like(mm)
+    ops.clip_head_fwd(img, txt, ls, img_n, txt_n, norms, mm, logits)
+    out = dict(img=img, txt=txt, ls=ls, img_n=img_n, txt_n=txt_n, norms=norms, logits=logits,
+               dmm=torch.empty_like(mm), cos_ws=torch.empty(2 * B, device=dev), loss=torch.empty(4, device=dev),
+               dimg_n=torch.empty_like(img), dtxt_n=torch.empty_like(txt), dimg=torch.empty_like(img),
+               dtxt=torch.empty_like(txt), soft_ws=torch.empty(2 * B * D, dtype=torch.float16, device=dev))
+    return out
+
+
+def _soft(h, q):
+    ops.clip_loss_soft_fwd_bwd(h["img"], h["txt"], h["img_n"], h["txt_n"], h["norms"], h["logits"], q, h["ls"],
+                               h["dmm"], h["cos_ws"], h["soft_ws"], h["loss"], h["dimg_n"], h["dtxt_n"], h["dimg"],
+                               h["dtxt"])
+
+
+@pytest.mark.parametrize("B,K", [(8, 38), (32, 10), (3, 100)])
+def test_clip_head_loss_soft(dev, B, K):
+    """Soft-label branch (trainers/maple.py:356-360) against an fp32 torch restatement:
+    KL(q.clamp(1e-8) || softmax(logits)) batchmean + 0.5 (1 - mean cos(img_n, q @ txt_n))."""
+    D = 512
+    h = _head_setup(dev, B, K, D, 7)
+    q = torch.rand(B, K, device=dev) ** 4
+    q[0, :] = 0.0
+    q[0, K // 2] = 1.0                      # a one-hot row (zeros clamp to 1e-8 inside the KL)
+    q = (q / q.sum(1, keepdim=True)).contiguous()
+    _soft(h, q)
+    i32 = h["img"].float().requires_grad_(True)
+    t32 = h["txt"].float().requires_grad_(True)
+    a = F.normalize(i32, dim=-1, eps=1e-8)
+    t = F.normalize(t32, dim=-1, eps=1e-8)
+    lg = h["ls"].exp().clamp(max=100) * (a @ t.t())
+    kl = F.kl_div(F.log_softmax(lg, dim=1), q.clamp(min=1e-8), reduction="batchmean")
+    tot = kl + 0.5 * (1 - F.cosine_similarity(a, q @ t).mean())
+    tot.backward()
+    loss = h["loss"].cpu()
+    assert loss[3].item() == 0.0
+    assert abs(loss[0].item() - tot.item()) < 5e-3, (loss[0].item(), tot.item())
+    assert abs(loss[1].item() - kl.item()) < 5e-3
+    torch.testing.assert_close(h["dimg"].float(), i32.grad, rtol=2e-2, atol=2e-4)
+    torch.testing.assert_close(h["dtxt"].float(), t32.grad, rtol=2e-2, atol=2e-4)
+
+
+def test_clip_head_loss_soft_onehot_matches_hard(dev):
+    """One-hot soft labels reproduce the cross-entropy branch: the KL of a one-hot target is the CE
+    (the 1e-8 clamps add < 1e-6), q @ txt_n selects txt_n[y] exactly, so the logit gradient and d img are
+    bit-identical; d txt differs only in where the per-row cosine gradients are rounded."""
+    B, K, D = 16, 38, 512
+    h = _head_setup(dev, B, K, D, 8)
+    y = torch.randint(0, K, (B,), device=dev)
+    y[0] = y[1]                              # two rows on one class
+    ops.clip_loss_fwd_bwd(h["img"], h["txt"], h["img_n"], h["txt_n"], h["norms"], h["logits"], y, h["ls"],
+                          h["dmm"], h["cos_ws"], h["loss"], h["dimg_n"], h["dtxt_n"], h["dimg"], h["dtxt"])
+    hard = {k: h[k].clone() for k in ("loss", "dmm", "dimg", "dtxt")}
+    _soft(h, F.one_hot(y, K).float().contiguous())
+    assert torch.equal(h["dmm"], hard["dmm"])
+    assert torch.equal(h["dimg"], hard["dimg"])
+    torch.testing.assert_close(h["dtxt"].float(), hard["dtxt"].float(), rtol=2e-3, atol=1e-6)
+    assert abs(h["loss"][1].item() - hard["loss"][1].item()) <= 2e-3      # CE is rounded to fp16
+    assert h["loss"][2].item() == hard["loss"][2].item()
+
 def test_sgd_and_clip(dev):
     torch.manual_seed(6)
     n16, n32 = 10000, 5000

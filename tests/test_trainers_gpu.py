@@ -68,3 +68,25 @@ def test_failed_client_is_excluded(dev, tmp_path):
     assert tr._fedavg([]) == 1
     for n, v in good.items():  # average of the single valid client = its own weights, fp16-rounded
         assert torch.equal(tr.clients[1].engine.P[n].float(), v.half().float()), n
+
+
+def test_soft_label_batches_through_the_trainer(dev, tmp_path):
+    """A batch with float labels [B, K] (mixup-style soft targets) takes the KL branch of the loss
+    (trainers/maple.py:356-360) through the client's forward_backward; each branch gets its own captured
+    step, and alternating branches keeps training finite."""
+    cfg = small_cfg(tmp_path, clients=1)
+    tr = build_trainer(cfg)
+    c = tr.clients[0]
+    batch = next(iter(c.dm.train_loader))
+    B, K = batch["label"].shape[0], c.engine.K
+    g = torch.Generator().manual_seed(3)
+    soft = torch.rand(B, K, generator=g)
+    soft = soft / soft.sum(1, keepdim=True)
+    sbatch = dict(batch, label=soft)
+    losses = [c.forward_backward(sbatch)["loss"], c.forward_backward(batch)["loss"],
+              c.forward_backward(sbatch)["loss"], c.forward_backward(batch)["loss"]]
+    assert set(c._graphs) == {False, True}
+    assert all(l == l and abs(l) < 1e3 for l in losses)
+    assert c.engine.soft_labels is False
+    with pytest.raises(ValueError):
+        c.forward_backward(dict(batch, label=soft[:, :-1].contiguous()))
