@@ -170,6 +170,24 @@ def main():
         fts.append(time.perf_counter() - a)
     fedavg_ms = 1e3 * float(np.median(fts))
 
+    # ---------------- eval (test() path, trainers/maple.py:660-681): logits + argmax per batch, with
+    # the class-prompt text features re-encoded per batch as the reference does, and cached across
+    # the pass (bit-identical logits)
+    acc = torch.zeros(2, device=dev)
+
+    def eval_rate(reuse, n=10):
+        load(0)
+        eng.eval_batch(batches[0][1], acc)  # encodes the text features once
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for i in range(n):
+            load(i)
+            eng.eval_batch(batches[i % 2][1], acc, reuse_text=reuse)
+        torch.cuda.synchronize()
+        return B * n / (time.perf_counter() - a)
+
+    eval_full, eval_cached = eval_rate(False), eval_rate(True)
+
     # ---------------- per-launch roofline of the dominant kernel (eager pass, HIP events on the
     # launching stream around every launch of that kernel during 2 full steps)
     # (towers serialised on one stream here so that no other kernel runs inside a probed launch)
@@ -246,6 +264,8 @@ def main():
                    "round": f"{args.steps} local steps + 1 FedAvg", "hipgraph": not args.no_graph},
         "fedavg_ms": fedavg_ms,
         "fedavg_valid_clients": fed.n_valid(),
+        "eval_images_per_s": {"text_reencoded_per_batch": eval_full, "text_cached_per_pass": eval_cached,
+                              "per_gpu": True},
         "model_tflops": world * step_flop * args.steps / elapsed / 1e12,
         "model_mfma_frac": world * step_flop * args.steps / elapsed / MFMA_PEAK_F16 / world,
         "loss": loss,

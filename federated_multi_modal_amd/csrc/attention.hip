@@ -516,56 +516,48 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd3_kernel(const f16* __rest
 // sum and the fp16 P pack then run from registers, and P . V follows.  Bit-identical to
 // attn_fwd_kernel (the same products in the same order; max is exact; the row sum and the P.V
 // accumulation keep its order) with a third fewer MFMAs and K reads and no per-chunk latency chain.
-template <int LKP, bool CAUSAL>
-__global__ __launch_bounds__(512, 4) void attn_fwd4_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
-                                                           f16* __restrict__ out, int64_t ld_out,
-                                                           float* __restrict__ lse, int ld_lse, int L, int H) {
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a constant)
+MF_DEV void wait_vmcnt(int n) {
+  switch (n) {
+    case 0: __builtin_amdgcn_s_waitcnt((0 & 15) | (7 << 4) | (15 << 8)); break;
+    case 1: __builtin_amdgcn_s_waitcnt((1 & 15) | (7 << 4) | (15 << 8)); break;
+    case 2: __builtin_amdgcn_s_waitcnt((2 & 15) | (7 << 4) | (15 << 8)); break;
+    case 3: __builtin_amdgcn_s_waitcnt((3 & 15) | (7 << 4) | (15 << 8)); break;
+    case 4: __builtin_amdgcn_s_waitcnt((4 & 15) | (7 << 4) | (15 << 8)); break;
+    case 5: __builtin_amdgcn_s_waitcnt((5 & 15) | (7 << 4) | (15 << 8)); break;
+    case 6: __builtin_amdgcn_s_waitcnt((6 & 15) | (7 << 4) | (15 << 8)); break;
+    default: __builtin_amdgcn_s_waitcnt((0 & 15) | (7 << 4) | (15 << 8)); break;
+  }
+}
+
+// One 16-query tile of attn_fwd4_kernel once its Q fragments are in registers: scores, softmax, P.V.
+// koff: [s2][hf] flattened (4), voff: [dt][hf] flattened (8).  V_WAIT: the V image may still be
+// landing; it is waited for (vmcnt 0 + workgroup barrier) between the softmax and P.V, so every wave
+// of the workgroup calls this, active or not.
+template <int LKP, bool CAUSAL, bool V_WAIT>
+MF_DEV void fwd4_tile(const f16* sK, const f16* sV, const int* koff, const int* voff, f16x8 qf0, f16x8 qf1,
+                      bool active, int q0, int L, int lane, f16* __restrict__ out, int64_t ld_out,
+                      float* __restrict__ lse, int ld_lse, int64_t row0, int h, int nh) {
   constexpr int NKT = LKP / 16;
   constexpr int NKS = LKP / 32;
-  __shared__ __attribute__((aligned(16))) f16 sK[LKP * 64];
-  __shared__ __attribute__((aligned(16))) f16 sV[LKP * 64];
-  const int D = H * 64;
-  const int nh = blockIdx.x, n = nh / H, h = nh % H;
-  const f16* base = qkv + (int64_t)n * L * ld_qkv;
-  stage_rows<LKP>(sK, base, ld_qkv, L, D + h * 64);
-  stage_rows<LKP>(sV, base, ld_qkv, L, 2 * D + h * 64);
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int fr = lane & 15, fg = lane >> 4, ii = lane & 15;
-  int koff[2][2], voff[4][2];
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const int row = 16 * hf + fr;
-      koff[s2][hf] = row * 64 + (((4 * s2 + fg) ^ (row & 7)) << 3);
-    }
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) voff[dt][hf] = sw_off(16 * hf + 4 * fg + (ii >> 2), 16 * dt + 4 * (ii & 3));
-  }
-  stage_wait();
-
-  for (int q0 = (blockIdx.y * nw + w) * 16; q0 < L; q0 += gridDim.y * nw * 16) {
-    const int q = q0 + fr;
-    const int qc = q < L ? q : L - 1;
-    f16x8 qf[2];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) qf[s2] = *(const f16x8*)(base + (int64_t)qc * ld_qkv + h * 64 + 32 * s2 + 8 * fg);
-    const int kt_end = CAUSAL ? min(NKT, (q0 + 16 + 15) / 16) : NKT;
-    const int ks_end = (kt_end + 1) / 2;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int q = q0 + fr;
+  const int kt_end = CAUSAL ? min(NKT, (q0 + 16 + 15) / 16) : NKT;
+  const int ks_end = (kt_end + 1) / 2;
+  f32x4 sc[NKS][2];
+  float m = -INFINITY;
+  if (active) {
     // all scores: S^T tiles (key rows, this lane's query column), chunk ks = keys 32ks .. 32ks+31
-    f32x4 sc[NKS][2];
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       sc[ks][0] = sc[ks][1] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
       if (ks < ks_end) {
         const f16* kb = sK + ks * 32 * 64;
         f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          a0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[s2][0]), qf[s2], a0, 0, 0, 0);
-          a1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[s2][1]), qf[s2], a1, 0, 0, 0);
-        }
+        a0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[0]), qf0, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[1]), qf0, a1, 0, 0, 0);
+        a0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[2]), qf1, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[3]), qf1, a1, 0, 0, 0);
         sc[ks][0] = a0;
         sc[ks][1] = a1;
       }
@@ -573,7 +565,6 @@ __global__ __launch_bounds__(512, 4) void attn_fwd4_kernel(const f16* __restrict
       // exceed the 128-VGPR budget of 16 waves per CU)
       if (ks & 1) asm volatile("" ::: "memory");
     }
-    float m = -INFINITY;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       if (ks < ks_end && (CAUSAL || 32 * ks + 32 > L)) {
@@ -589,48 +580,109 @@ __global__ __launch_bounds__(512, 4) void attn_fwd4_kernel(const f16* __restrict
     }
     m = fmaxf(m, __shfl_xor(m, 16, 64));
     m = fmaxf(m, __shfl_xor(m, 32, 64));
-    constexpr float kLog2eScale = 0.125f * 1.4426950408889634f;
-    const float mb = -m * kLog2eScale;
-    float l = 0.f;
-    f32x4 oacc[4];
+  }
+  if (V_WAIT) stage_wait();  // V landed (this wave's DMA, then every wave's)
+  if (!active) return;
+  constexpr float kLog2eScale = 0.125f * 1.4426950408889634f;
+  const float mb = -m * kLog2eScale;
+  float l = 0.f;
+  f32x4 oacc[4];
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) oacc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int dt = 0; dt < 4; ++dt) oacc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      if (ks < ks_end) {
-        f16x8 pf;
+  for (int ks = 0; ks < NKS; ++ks) {
+    if (ks < ks_end) {
+      f16x8 pf;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[ks][0][i], kLog2eScale, mb));
-          const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[ks][1][i], kLog2eScale, mb));
-          l += p0 + p1;
-          pf[i] = (f16)p0;
-          pf[4 + i] = (f16)p1;
-        }
-        const f16* vb = sV + ks * 32 * 64;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[dt][0]));
-          s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[dt][1]));
-          oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cat8(__builtin_bit_cast(f16x4, v0), __builtin_bit_cast(f16x4, v1)),
-                                                            pf, oacc[dt], 0, 0, 0);
-        }
+      for (int i = 0; i < 4; ++i) {
+        const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[ks][0][i], kLog2eScale, mb));
+        const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[ks][1][i], kLog2eScale, mb));
+        l += p0 + p1;
+        pf[i] = (f16)p0;
+        pf[4 + i] = (f16)p1;
       }
-    }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    if (q < L) {
-      const float inv = 1.0f / l;
-      f16* orow = out + ((int64_t)n * L + q) * ld_out + h * 64;
+      const f16* vb = sV + ks * 32 * 64;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        f16x4 o;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = (f16)(oacc[dt][i] * inv);
-        *(f16x4*)(orow + 16 * dt + 4 * fg) = o;
+        s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[2 * dt]));
+        s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[2 * dt + 1]));
+        oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cat8(__builtin_bit_cast(f16x4, v0), __builtin_bit_cast(f16x4, v1)),
+                                                          pf, oacc[dt], 0, 0, 0);
       }
-      if (fg == 0) lse[(int64_t)nh * ld_lse + q] = m * kScale + __logf(l);
     }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (q < L) {
+    const float inv = 1.0f / l;
+    f16* orow = out + (row0 + q) * ld_out + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f16x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = (f16)(oacc[dt][i] * inv);
+      *(f16x4*)(orow + 16 * dt + 4 * fg) = o;
+    }
+    if (fg == 0) lse[(int64_t)nh * ld_lse + q] = m * kScale + __logf(l);
+  }
+}
+
+// Forward, single pass with register-resident scores: the grid / wave layout of attn_fwd_kernel
+// (16 queries per wave), but every score of the wave's queries (LKP keys x 16 queries = LKP/4 fp32 per
+// lane) is computed ONCE by independent back-to-back MFMAs and kept in registers; row max, exp, row
+// sum and the fp16 P pack then run from registers, and P . V follows.  Bit-identical to
+// attn_fwd_kernel (the same products in the same order; max is exact; the row sum and the P.V
+// accumulation keep its order) with a third fewer MFMAs and K reads and no per-chunk latency chain.
+// Staging overlaps the first tile: its Q fragments are loaded first, then K, then V (LDS-DMA); the
+// scores start once Q and K have landed (vmcnt = this wave's V loads) and V is waited for only before
+// P.V, so the V transfer runs under the score MFMAs and the softmax.
+template <int LKP, bool CAUSAL>
+__global__ __launch_bounds__(512, 4) void attn_fwd4_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
+                                                           f16* __restrict__ out, int64_t ld_out,
+                                                           float* __restrict__ lse, int ld_lse, int L, int H) {
+  __shared__ __attribute__((aligned(16))) f16 sK[LKP * 64];
+  __shared__ __attribute__((aligned(16))) f16 sV[LKP * 64];
+  const int D = H * 64;
+  const int nh = blockIdx.x, n = nh / H, h = nh % H;
+  const f16* base = qkv + (int64_t)n * L * ld_qkv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4, ii = lane & 15;
+  const int qstep = gridDim.y * nw * 16;
+  int q0 = (blockIdx.y * nw + w) * 16;
+  const bool active = q0 < L;
+  f16x8 qf0, qf1;
+  {
+    const int q = q0 + fr;
+    const f16* qrow = base + (int64_t)(q < L ? q : L - 1) * ld_qkv + h * 64 + 8 * fg;
+    qf0 = *(const f16x8*)qrow;
+    qf1 = *(const f16x8*)(qrow + 32);
+  }
+  stage_rows<LKP>(sK, base, ld_qkv, L, D + h * 64);
+  stage_rows<LKP>(sV, base, ld_qkv, L, 2 * D + h * 64);
+  const int nv = w < LKP / 8 ? (LKP / 8 - w + nw - 1) / nw : 0;  // this wave's V loads (issued last)
+
+  int koff[4], voff[8];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int row = 16 * hf + fr;
+      koff[2 * s2 + hf] = row * 64 + (((4 * s2 + fg) ^ (row & 7)) << 3);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) voff[2 * dt + hf] = sw_off(16 * hf + 4 * fg + (ii >> 2), 16 * dt + 4 * (ii & 3));
+  }
+  wait_vmcnt(nv);   // Q and this wave's K landed
+  __syncthreads();  // ... and every wave's K
+  fwd4_tile<LKP, CAUSAL, true>(sK, sV, koff, voff, qf0, qf1, active, q0, L, lane, out, ld_out, lse, ld_lse,
+                               (int64_t)n * L, h, nh);
+  for (q0 += qstep; q0 < L; q0 += qstep) {
+    const int q = q0 + fr;
+    const f16* qrow = base + (int64_t)(q < L ? q : L - 1) * ld_qkv + h * 64 + 8 * fg;
+    qf0 = *(const f16x8*)qrow;
+    qf1 = *(const f16x8*)(qrow + 32);
+    fwd4_tile<LKP, CAUSAL, false>(sK, sV, koff, voff, qf0, qf1, true, q0, L, lane, out, ld_out, lse, ld_lse,
+                                  (int64_t)n * L, h, nh);
   }
 }
 
@@ -1065,7 +1117,9 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
   hipStream_t st = (hipStream_t)stream;
   static const int fwd_variant = getenv("MAPFED_ATTN_FWD") ? atoi(getenv("MAPFED_ATTN_FWD")) : 4;  // A/B knob
   if (fwd_variant == 4) {
-    const dim3 grid4(N * H, attn_qsplit(N * H, L)), block4(attn_threads(L));
+    // the head's 16-query tiles split evenly over its workgroups (no workgroup without a tile)
+    const int qs4 = attn_qsplit(N * H, L), tiles = (L + 15) / 16;
+    const dim3 grid4(N * H, qs4), block4(64 * std::min(8, (tiles + qs4 - 1) / qs4));
 #define CALLF4(P)                                                                                             \
   if (causal)                                                                                                 \
     attn_fwd4_kernel<P, true><<<grid4, block4, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); \

@@ -514,26 +514,36 @@ class MapleEngine:
                           self.post_mean, self.post_rstd, row_index=self.cls_rows)
         ops.gemm(self.vis_post, P["image_encoder.proj"], self.img_feat, epilogue=ops.EPI_NONE, b_kmajor=True)
 
-    def eval_batch(self, labels: Optional[torch.Tensor], acc: torch.Tensor, pred: Optional[torch.Tensor] = None):
+    def eval_batch(self, labels: Optional[torch.Tensor], acc: torch.Tensor, pred: Optional[torch.Tensor] = None,
+                   reuse_text: bool = False):
         """One test batch (trainers/maple.py:671-677): logits, argmax, correct count accumulated in
-        acc (device float[2]: correct, total).  Images must already be in img_in."""
-        logits = self.forward()
+        acc (device float[2]: correct, total).  Images must already be in img_in.  reuse_text: see
+        forward()."""
+        logits = self.forward(reuse_text=reuse_text)
         ops.argmax_correct(logits, labels, pred, acc)
         return logits
 
-    def forward(self):
+    def forward(self, reuse_text: bool = False):
         """CustomCLIP.forward up to the logits (eval path, trainers/maple.py:304-346).  The text and
         vision towers are independent until the head: the text tower runs on a side stream, forked
         from and joined back into the current stream (also inside a captured hipGraph), so its
-        smaller kernels fill the CUs the vision GEMMs leave idle."""
+        smaller kernels fill the CUs the vision GEMMs leave idle.
+
+        reuse_text=True keeps the text features of the previous forward: the
+        reference re-encodes every class prompt for every test batch (trainers/maple.py:329 under
+        test(), :660-681), although they depend on the weights only.  Within a test pass the weights
+        are fixed and the text tower is deterministic, so the cached features are bit-identical to
+        recomputed ones; the caller must not set it after a weight change."""
         self._prompt_learner_fwd()
         main = torch.cuda.current_stream(self.device)
-        side = self.side if self.overlap_towers else main
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            self._text_forward()
+        side = self.side if (self.overlap_towers and not reuse_text) else main
+        if not reuse_text:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self._text_forward()
         self._vision_forward()
-        main.wait_stream(side)
+        if not reuse_text:
+            main.wait_stream(side)
         ops.clip_head_fwd(self.img_feat, self.txt_feat, self.P["logit_scale"], self.img_n, self.txt_n, self.norms,
                           self.mm, self.logits)
         return self.logits

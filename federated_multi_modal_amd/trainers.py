@@ -288,17 +288,21 @@ class MaPLe(TrainerX):
         loader = self.dm.test_loader
         ev = self._evaluator(loader.batch)
         self._acc.zero_()
+        # the class-prompt text features depend on the weights only: encoded by the first batch and
+        # reused by the rest of the pass (bit-identical)
+        reuse = False
         for batch in loader:
             x, y, _ = self.parse_batch_train(batch)
             n = y.numel()
             if n == ev.B:
                 ev.img_in.copy_(x)
-                ev.eval_batch(y, self._acc)
+                ev.eval_batch(y, self._acc, reuse_text=reuse)
             else:  # ragged last batch: pad the static buffer, count only the real rows
                 ev.img_in.zero_()
                 ev.img_in[:n].copy_(x)
-                logits = ev.forward()
+                logits = ev.forward(reuse_text=reuse)
                 ops.argmax_correct(logits[:n], y, None, self._acc)
+            reuse = True
         correct, total = self._acc.tolist()
         acc = 100.0 * correct / total if total > 0 else 0.0
         print(f"[Client {self.client_id}] Test Accuracy: {acc:.2f}%")

@@ -193,3 +193,21 @@ def test_engine_soft_labels_vs_oracle(dev):
     # switching back to integer labels returns to the cross-entropy branch
     e.load_batch(torch.from_numpy(batch.images), torch.from_numpy(batch.labels))
     assert not e.soft_labels
+
+
+def test_eval_reuses_text_features_bit_exactly(dev):
+    """Eval with the class-prompt text features cached across test batches:
+    the logits of a second batch equal a full forward (text re-encoded) bit for bit."""
+    J, K, B, seed = 3, 10, 4, 2
+    names = syn.synthetic_classnames(K, seed)
+    e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed), device=dev)
+    b0, b1 = syn.client_batch(seed, 0, 0, B, K), syn.client_batch(seed, 0, 1, B, K)
+    e.load_batch(torch.from_numpy(b0.images))
+    e.forward()
+    e.load_batch(torch.from_numpy(b1.images))
+    cached = e.forward(reuse_text=True).clone()
+    full = e.forward().clone()
+    assert torch.equal(cached, full)
+    acc = torch.zeros(2, device=dev)
+    e.eval_batch(torch.from_numpy(b1.labels).to(dev), acc, reuse_text=True)
+    assert acc[1].item() == B
