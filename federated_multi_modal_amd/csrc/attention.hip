@@ -539,7 +539,8 @@ MF_DEV void fwd4_tile(const f16* sK, const f16* sV, const int* koff, const int* 
                       bool active, int q0, int L, int lane, f16* __restrict__ out, int64_t ld_out,
                       float* __restrict__ lse, int ld_lse, int64_t row0, int h, int nh) {
   constexpr int NKT = LKP / 16;
-  constexpr int NKS = LKP / 32;
+  constexpr int NKS = (LKP + 31) / 32;
+  constexpr bool HALF = (LKP % 32) != 0;  // the last 32-key chunk has only its first 16 keys staged
   const int fr = lane & 15, fg = lane >> 4;
   const int q = q0 + fr;
   const int kt_end = CAUSAL ? min(NKT, (q0 + 16 + 15) / 16) : NKT;
@@ -555,11 +556,13 @@ MF_DEV void fwd4_tile(const f16* sK, const f16* sV, const int* koff, const int* 
         const f16* kb = sK + ks * 32 * 64;
         f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
         a0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[0]), qf0, a0, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[1]), qf0, a1, 0, 0, 0);
         a0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[2]), qf1, a0, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[3]), qf1, a1, 0, 0, 0);
         sc[ks][0] = a0;
-        sc[ks][1] = a1;
+        if (!(HALF && ks == NKS - 1)) {  // keys 32ks+16.. exist (else they stay -inf: P = 0)
+          a1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[1]), qf0, a1, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[3]), qf1, a1, 0, 0, 0);
+          sc[ks][1] = a1;
+        }
       }
       // keep at most two chunks of K fragments in flight (the compiler would hoist every read and
       // exceed the 128-VGPR budget of 16 waves per CU)
@@ -605,7 +608,9 @@ MF_DEV void fwd4_tile(const f16* sK, const f16* sV, const int* koff, const int* 
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[2 * dt]));
-        s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[2 * dt + 1]));
+        s16x4 v1 = {0, 0, 0, 0};  // unstaged keys of a half chunk: V = 0 against P = 0
+        if (!(HALF && ks == NKS - 1))
+          v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[2 * dt + 1]));
         oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cat8(__builtin_bit_cast(f16x4, v0), __builtin_bit_cast(f16x4, v1)),
                                                           pf, oacc[dt], 0, 0, 0);
       }
@@ -1120,12 +1125,23 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
     // the head's 16-query tiles split evenly over its workgroups (no workgroup without a tile)
     const int qs4 = attn_qsplit(N * H, L), tiles = (L + 15) / 16;
     const dim3 grid4(N * H, qs4), block4(64 * std::min(8, (tiles + qs4 - 1) / qs4));
+    const int LP16 = tiles * 16;  // keys staged in 16-row tiles (LP16 % 32 == 16: a half last chunk)
 #define CALLF4(P)                                                                                             \
   if (causal)                                                                                                 \
     attn_fwd4_kernel<P, true><<<grid4, block4, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); \
   else                                                                                                        \
     attn_fwd4_kernel<P, false><<<grid4, block4, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H);
-    MF_ATTN_DISPATCH(LP, CALLF4)
+    switch (LP16) {
+      case 16: CALLF4(16); break;
+      case 48: CALLF4(48); break;
+      case 80: CALLF4(80); break;
+      case 112: CALLF4(112); break;
+      case 144: CALLF4(144); break;
+      case 176: CALLF4(176); break;
+      case 208: CALLF4(208); break;
+      case 240: CALLF4(240); break;
+      default: MF_ATTN_DISPATCH(LP, CALLF4)
+    }
 #undef CALLF4
     MF_CHECK_LAUNCH();
     return 0;

@@ -47,6 +47,12 @@ class EngineConfig:
     momentum: float = 0.9       # Dassl SGD defaults (cfg.OPTIM.MOMENTUM / WEIGHT_DECAY)
     weight_decay: float = 5e-4
     max_grad_norm: float = 1.0
+    # Run the text tower on the first max(EOT)+1 tokens instead of all 77 (SURVEY.md §8(d) optional
+    # mode, reported separately).  Under the causal mask a token only sees earlier ones, and the tower's
+    # output is gathered at the EOT row, so the dropped tokens cannot reach the loss: the forward is
+    # bit-identical, the backward differs only in fp32 summation order (zero rows fewer in the weight
+    # gradients' reductions).  Off by default: the reference computes all 77.
+    eot_truncate: bool = False
 
 
 def _is_trainable(name: str) -> bool:
@@ -273,15 +279,17 @@ class MapleEngine:
             self.hyper = torch.tensor([0.0, cfg.momentum, cfg.weight_decay, 1.0], device=self.device, dtype=F32)
         else:
             assert shared.K == self.K and shared.J == self.J and shared.device == self.device
+            assert shared.cfg.eot_truncate == cfg.eot_truncate
             for a in ("n16", "n32", "flat16", "flat32", "gflat16", "gflat32", "mom16", "mom32", "P", "G",
-                      "trainable_names", "conv_w", "chunks", "nchunks", "norm_part", "clip_out", "WT", "tokenized", "token_prefix", "token_suffix", "eot_rows", "hyper"):
+                      "trainable_names", "conv_w", "chunks", "nchunks", "norm_part", "clip_out", "WT", "tokenized",
+                      "token_prefix", "token_suffix", "token_suffix_run", "text_len", "eot_rows", "hyper"):
                 setattr(self, a, getattr(shared, a))
         G2 = d.grid * d.grid
         self.Lv = G2 + 1 + cfg.n_ctx
         self.G2 = G2
         self.vis = _Tower(self, "image_encoder", self.B, self.Lv, d.vision_width, d.vision_heads, d.vision_layers,
                           False, G2 + 1)
-        self.txt = _Tower(self, "text_encoder", self.K, d.context_length, d.text_width, d.text_heads, d.text_layers,
+        self.txt = _Tower(self, "text_encoder", self.K, self.text_len, d.text_width, d.text_heads, d.text_layers,
                           True, 1)
         self._build_io()
         self.side = torch.cuda.Stream(device=self.device)
@@ -376,14 +384,31 @@ class MapleEngine:
         self.token_prefix = torch.from_numpy(emb[:, :1]).to(dev, F16).contiguous()
         self.token_suffix = torch.from_numpy(emb[:, 1 + cfg.n_ctx:]).to(dev, F16).contiguous()
         eot = tok.argmax(axis=-1)
-        self.eot_rows = torch.from_numpy((np.arange(len(texts)) * 77 + eot).astype(np.int32)).to(dev)
+        L = cfg.dims.context_length
+        self.text_len = max(int(eot.max()) + 1, 1 + cfg.n_ctx) if cfg.eot_truncate else L
+        self.eot_rows = torch.empty(len(texts), device=dev, dtype=torch.int32)
+        self.token_suffix_run = self.token_suffix
+        self._refresh_text_run(eot)
+
+    def _refresh_text_run(self, eot: np.ndarray):
+        """EOT gather rows and the suffix rows the text tower runs on (all 77 tokens, or the first
+        text_len under eot_truncate; the assemble kernel reads a contiguous [K, text_len-1-n_ctx, D])."""
+        Lt, n_ctx = self.text_len, self.cfg.n_ctx
+        if int(eot.max()) >= Lt:
+            raise ValueError(f"EOT at token {int(eot.max())} beyond the {Lt} tokens the text tower runs on")
+        self.eot_rows.copy_(torch.from_numpy((np.arange(len(eot)) * Lt + eot).astype(np.int32)))
+        if Lt != self.cfg.dims.context_length:
+            run = self.token_suffix[:, :Lt - 1 - n_ctx].contiguous()
+            if self.token_suffix_run is self.token_suffix or self.token_suffix_run.shape != run.shape:
+                self.token_suffix_run = run
+            else:
+                self.token_suffix_run.copy_(run)
 
     def set_text_prompts(self, token_prefix: torch.Tensor, token_suffix: torch.Tensor, tokenized: torch.Tensor):
         """Use real tokenizer output (prefix/suffix embeddings as the reference registers them)."""
         self.token_prefix.copy_(token_prefix)
         self.token_suffix.copy_(token_suffix)
-        eot = tokenized.argmax(dim=-1).cpu().numpy()
-        self.eot_rows.copy_(torch.from_numpy((np.arange(len(eot)) * 77 + eot).astype(np.int32)))
+        self._refresh_text_run(tokenized.argmax(dim=-1).cpu().numpy())
 
     # ------------------------------------------------------------------ activations / io
     def _build_io(self):
@@ -492,7 +517,7 @@ class MapleEngine:
     def _text_forward(self):
         P = self.P
         t = self.txt
-        ops.text_assemble(self.token_prefix, P["prompt_learner.ctx"], self.token_suffix,
+        ops.text_assemble(self.token_prefix, P["prompt_learner.ctx"], self.token_suffix_run,
                           P["text_encoder.positional_embedding"], t.X[0], self.K, t.L, N_CTX, t.D)
         t.forward(self.txt_deep)
         ops.layernorm_fwd(t.X[-1], P["text_encoder.ln_final.weight"], P["text_encoder.ln_final.bias"], self.txt_final,
@@ -677,6 +702,7 @@ class MapleEngine:
             if "prompt_learner.token_prefix" in sd:
                 self.token_prefix.copy_(sd["prompt_learner.token_prefix"])
                 self.token_suffix.copy_(sd["prompt_learner.token_suffix"])
+                self._refresh_text_run(self.tokenized.argmax(dim=-1).numpy())
         self.refresh_transposes(all_layers=frozen_changed)
 
     def trainable_state(self) -> Dict[str, torch.Tensor]:

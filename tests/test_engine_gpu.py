@@ -211,3 +211,26 @@ def test_eval_reuses_text_features_bit_exactly(dev):
     acc = torch.zeros(2, device=dev)
     e.eval_batch(torch.from_numpy(b1.labels).to(dev), acc, reuse_text=True)
     assert acc[1].item() == B
+
+
+def test_eot_truncated_text_tower_matches_full(dev):
+    """Optional mode: the text tower on the first max(EOT)+1 tokens.  Logits and the
+    loss are bit-identical to the 77-token tower; gradients agree up to fp32 summation order."""
+    J, K, B, seed = 3, 10, 4, 4
+    names = syn.synthetic_classnames(K, seed)
+    b = syn.client_batch(seed, 0, 0, B, K)
+    out = []
+    for trunc in (False, True):
+        e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed, eot_truncate=trunc),
+                        device=dev)
+        e.load_batch(torch.from_numpy(b.images), torch.from_numpy(b.labels))
+        logits = e.forward().clone()
+        e.forward_backward()
+        out.append((e.text_len, logits, e.loss(), {k: v.detach().double().clone() for k, v in e.grads().items()}))
+    (l77, lg0, loss0, g0), (lt, lg1, loss1, g1) = out
+    assert l77 == 77 and lt < 77
+    assert torch.equal(lg0, lg1)
+    assert loss0 == loss1
+    worst = max(((g1[n] - g0[n]).norm() / (g0[n].norm() + 1e-30)).item() for n in g0)
+    print(f"text_len {lt}: worst grad rel diff {worst:.2e}")
+    assert worst <= 1e-2
