@@ -36,11 +36,13 @@ SIGNATURES = {
     "mf_cast_f16_f32": [P, P, L, P],
     "mf_small_linear_fwd": [P, P, P, P, I, I, I, I, P],
     "mf_small_linear_bwd": [P, P, P, P, P, P, I, I, I, I, I, P],
+    "mf_gemm_splitk_ws_floats": [I, I, I, I],
     "mf_small_linear_desc_bytes": [],
     "mf_small_linear_fwd_batch": [P, I, I, P],
     "mf_small_linear_bwd_batch": [P, I, I, I, I, P],
     "mf_clip_head_fwd": [P, P, I, I, I, P, P, P, P, P, P, P],
     "mf_clip_loss_fwd_bwd": [P, P, P, P, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P],
+    "mf_gemm_splitk": [P, L, I, P, L, I, P, L, I, I, I, P, L, I, I, P],
     "mf_clip_loss_soft_fwd_bwd": [P, P, P, P, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P],
     "mf_argmax_correct": [P, I, I, P, P, P, P],
     "mf_optim_chunk_bytes": [],
@@ -53,7 +55,8 @@ SIGNATURES = {
 }
 # functions that return a value, not a status
 _VALUE_FUNCS = {"mf_abi_version", "mf_layernorm_bwd_blocks", "mf_colsum_blocks", "mf_optim_chunk_bytes",
-                "mf_optim_chunk_elems", "mf_col_reduce_desc_bytes", "mf_small_linear_desc_bytes"}
+                "mf_optim_chunk_elems", "mf_col_reduce_desc_bytes", "mf_small_linear_desc_bytes",
+                "mf_gemm_splitk_ws_floats"}
 
 _LIB = None
 

@@ -15,6 +15,7 @@
 // one barrier per K-step; XCD-aware bijective block remap so tiles sharing an A panel share
 // an L2.  The MFMA is issued "swapped" (weight fragment as the A operand) so each lane ends with
 // 4 consecutive output columns of one row -> 8-byte stores.
+#include <algorithm>
 #include <type_traits>
 
 #include "mf_common.h"
@@ -40,7 +41,8 @@ struct GemmArgs {
   f16* aux_out;
   int64_t lda, ldb, ldc, ld_aux;
   int M, N, K;
-  int vec8;  // C / aux row strides are multiples of 8 elements -> 16-byte epilogue accesses
+  int vec8;    // C / aux row strides are multiples of 8 elements -> 16-byte epilogue accesses
+  int ksplit;  // > 0: split-K slice of ksplit (multiple of 64) per blockIdx.z, fp32 partial at C + z*M*ldc
 };
 
 // Elementwise epilogue on 8 consecutive columns (fp16 staged value t = the GEMM result rounded at
@@ -300,7 +302,15 @@ MF_DEV void dma_stage(const f16* A, int a_bytes, const f16* B, int b_bytes, f16*
 }
 
 template <int BM, int BN, int WM, int WN, int S, int EPI, bool TA = false, bool TB = false>
-__global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g) {
+__global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g0) {
+  GemmArgs g = g0;
+  if (g.ksplit > 0) {  // split-K: this workgroup's K slice and partial-sum plane (EPI_F32)
+    const int k0 = blockIdx.z * g.ksplit;
+    g.A += (int64_t)k0 * (TA ? g.lda : 1);
+    g.B += (int64_t)k0 * (TB ? g.ldb : 1);
+    g.K = min(g.ksplit, g.K - k0);
+    g.C = (float*)g.C + (int64_t)blockIdx.z * g.M * g.ldc;
+  }
   constexpr int NW = WM * WN;
   constexpr int NT = NW * 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;  // per-wave tile
@@ -603,7 +613,8 @@ int launch_tile8(const GemmArgs& a, int epi, hipStream_t st) {
 template <int BM, int BN, int WM, int WN, int S, bool TA = false, bool TB = false>
 int launch_tile(const GemmArgs& a, int epi, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  dim3 grid(tiles), block(WM * WN * 64);
+  const int splits = a.ksplit > 0 ? (a.K + a.ksplit - 1) / a.ksplit : 1;
+  dim3 grid(tiles, 1, splits), block(WM * WN * 64);
   switch (epi) {
     case EPI_NONE: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_NONE, TA, TB><<<grid, block, 0, st>>>(a); break;
     case EPI_BIAS: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_BIAS, TA, TB><<<grid, block, 0, st>>>(a); break;
@@ -635,6 +646,33 @@ int launch_kmajor(const GemmArgs& a, bool ta, bool tb, int epi, int tile, hipStr
 #undef MF_KM
 }
 
+// automatic split count (tests/diagnostics/splitk_bench.py on the MaPLe dW shapes, K = 2926..6368):
+// >= 144 128x128 tiles run best unsplit; 64..143 tiles on 4 slices; fewer on 8
+inline int splitk_auto(int64_t tiles) { return tiles >= 144 ? 1 : (tiles >= 64 ? 4 : 8); }
+
+// split-K combine: C[m][n] = sum_{s=0..S-1} ws[s][m][n] in that order (deterministic), fp16 or fp32 out.
+// 4 columns per thread (N % 4 == 0).
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int S, int M, int N, void* __restrict__ C,
+                                     int64_t ldc, int out_f16) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nq = (int64_t)M * (N / 4);
+  if (t >= nq) return;
+  const int64_t m = t / (N / 4);
+  const int n = (int)(t % (N / 4)) * 4;
+  const int64_t plane = (int64_t)M * N;
+  f32x4 acc = *(const f32x4*)(ws + m * N + n);
+  for (int z = 1; z < S; ++z) {
+    const f32x4 v = *(const f32x4*)(ws + z * plane + m * N + n);
+    acc = (f32x4){acc[0] + v[0], acc[1] + v[1], acc[2] + v[2], acc[3] + v[3]};
+  }
+  if (out_f16) {
+    f16x4 o = {(f16)acc[0], (f16)acc[1], (f16)acc[2], (f16)acc[3]};
+    *(f16x4*)((f16*)C + m * ldc + n) = o;
+  } else {
+    *(f32x4*)((float*)C + m * ldc + n) = acc;
+  }
+}
+
 }  // namespace
 
 // C[M,N] = epilogue(op(A) . op(B)^T):  a_kmajor = 0: A[m][k] at A[m*lda + k], 1: A[k*lda + m];
@@ -659,7 +697,7 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
   const int vec8 = (ldc % 8 == 0) && (ld_aux % 8 == 0) && ((uintptr_t)C % 16 == 0) &&
                    (!aux_in || (uintptr_t)aux_in % 16 == 0) && (!aux_out || (uintptr_t)aux_out % 16 == 0);
   GemmArgs a{(const f16*)A, (const f16*)B, C, (const f16*)bias, (const f16*)aux_in, (f16*)aux_out,
-             lda, ldb, ldc, ld_aux, M, N, K, vec8};
+             lda, ldb, ldc, ld_aux, M, N, K, vec8, 0};
   hipStream_t st = (hipStream_t)stream;
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   if (a_kmajor || b_kmajor) {
@@ -693,4 +731,51 @@ extern "C" int mf_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb
                           int N, int K, const void* bias, const void* aux_in, void* aux_out, int64_t ld_aux,
                           int epilogue, int tile, void* stream) {
   return mf_gemm(A, lda, 0, B, ldb, 0, C, ldc, M, N, K, bias, aux_in, aux_out, ld_aux, epilogue, tile, stream);
+}
+
+// Split-K plain product C = op(A) . op(B)^T for few output tiles and a long K (the weight gradients
+// dW = dY^T X, K = tokens): `splits` workgroups per 128x128 tile each reduce a K slice into an fp32
+// plane of ws (splits * M * N floats), then one pass sums the planes in a fixed order into C (fp16
+// when out_f16, else fp32).  splits <= 0 picks enough slices for ~2 workgroups per CU.
+extern "C" int mf_gemm_splitk(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb, int b_kmajor,
+                              void* C, int64_t ldc, int M, int N, int K, float* ws, int64_t ws_floats, int splits,
+                              int out_f16, void* stream) {
+  if (M <= 0 || N <= 0) return 0;
+  const bool both_k = a_kmajor && b_kmajor;
+  if (K <= 0 || (!both_k && (K % BK) != 0))
+    return mf_set_error("mf_gemm_splitk: K must be a positive multiple of 64 unless both operands are K-major", -1);
+  if ((N % 8) != 0 || (lda % 8) || (ldb % 8) || (ldc % 4)) return mf_set_error("mf_gemm_splitk: alignment", -1);
+  if ((a_kmajor && (M % 8 || lda < M)) || (b_kmajor && (N % 8 || ldb < N)) || (!a_kmajor && lda < K) ||
+      (!b_kmajor && ldb < K))
+    return mf_set_error("mf_gemm_splitk: K-major operands need rows % 8 == 0 and ld >= rows; row-major ld >= K", -1);
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)ws % 16 || (uintptr_t)C % 16)
+    return mf_set_error("mf_gemm_splitk: pointers must be 16-byte aligned", -1);
+  const int64_t tiles = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
+  if (splits <= 0) splits = splitk_auto(tiles);
+  int ks = (int)((((int64_t)K + splits - 1) / splits + BK - 1) / BK * BK);
+  if (ks < BK) ks = BK;
+  splits = (K + ks - 1) / ks;
+  if ((int64_t)splits * M * N > ws_floats) return mf_set_error("mf_gemm_splitk: workspace too small", -1);
+  hipStream_t st = (hipStream_t)stream;
+  GemmArgs a{(const f16*)A, (const f16*)B, ws, nullptr, nullptr, nullptr, lda, ldb, (int64_t)N, 0, M, N, K, 1, ks};
+  int rc;
+  if (a_kmajor && b_kmajor) rc = launch_tile<128, 128, 2, 2, 2, true, true>(a, EPI_F32, st);
+  else if (a_kmajor) rc = launch_tile<128, 128, 2, 2, 2, true, false>(a, EPI_F32, st);
+  else if (b_kmajor) rc = launch_tile<128, 128, 2, 2, 2, false, true>(a, EPI_F32, st);
+  else rc = launch_tile<128, 128, 2, 2, 2>(a, EPI_F32, st);
+  if (rc) return rc;
+  const int64_t nq = (int64_t)M * (N / 4);
+  splitk_reduce_kernel<<<(unsigned)((nq + 255) / 256), 256, 0, st>>>(ws, splits, M, N, C, ldc, out_f16);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_gemm_splitk_ws_floats(int M, int N, int K, int splits) {
+  const int64_t tiles = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
+  if (splits <= 0) splits = splitk_auto(tiles);
+  int ks = (int)((((int64_t)K + splits - 1) / splits + BK - 1) / BK * BK);
+  if (ks < BK) ks = BK;
+  splits = (K + ks - 1) / ks;
+  const int64_t n = (int64_t)splits * M * N;
+  return n > 0x7fffffff ? -1 : (int)n;
 }

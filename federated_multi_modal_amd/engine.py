@@ -22,6 +22,7 @@ streaming kernels and FedAvg is one RCCL all-reduce of one contiguous bucket.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -184,6 +185,14 @@ class _Tower:
         self.dF = e(R, 4 * D)
         self.attn_ws = e(N * H * L, dt=F32)
         self.cs_ws = e(ops.colsum_ws_floats(R, 4 * D), dt=F32)
+        # split-K weight gradients of the trainable block (few output tiles, K = R tokens): fp32 partial
+        # planes, summed in a fixed order (MAPFED_DW_SPLITK=0: the single-pass K-major GEMM)
+        # (only where the automatic split count exceeds 1: few 128x128 output tiles)
+        use = os.environ.get("MAPFED_DW_SPLITK", "1") != "0"
+        shapes = ((3 * D, D), (D, D), (4 * D, D), (D, 4 * D))
+        ws = {s: ops.gemm_splitk_ws_floats(s[0], s[1], R) for s in shapes}
+        self.dw_split = {s for s in shapes if use and ws[s] > s[0] * s[1]}
+        self.dw_ws = e(max(ws[s] for s in self.dw_split), dt=F32) if self.dw_split else None
 
     # -- parameters of block i
     def p(self, i: int, key: str) -> torch.Tensor:
@@ -221,7 +230,10 @@ class _Tower:
 
     def _dw(self, dY: torch.Tensor, Xin: torch.Tensor, dW: torch.Tensor, db: torch.Tensor):
         """dW[out,in] = dY^T . Xin (fp16 out; both operands read K-major in place, K = rows), db = colsum(dY)."""
-        ops.gemm(dY, Xin, dW, epilogue=ops.EPI_NONE, a_kmajor=True, b_kmajor=True)
+        if tuple(dW.shape) in self.dw_split:
+            ops.gemm_splitk(dY, Xin, dW, self.dw_ws, a_kmajor=True, b_kmajor=True)
+        else:
+            ops.gemm(dY, Xin, dW, epilogue=ops.EPI_NONE, a_kmajor=True, b_kmajor=True)
         ops.colsum(dY, db, self.cs_ws)
 
     def backward(self, n_prompted: int, prompt_grads: List[torch.Tensor]):

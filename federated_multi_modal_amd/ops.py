@@ -115,6 +115,32 @@ def gemm(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NONE, 
     return C
 
 
+
+def gemm_splitk_ws_floats(M: int, N: int, K: int, splits: int = 0) -> int:
+    n = call("mf_gemm_splitk_ws_floats", M, N, K, splits)
+    if n < 0:
+        raise ValueError("split-K workspace exceeds 2^31 floats")
+    return n
+
+
+def gemm_splitk(A, B, C, ws, splits=0, a_kmajor=False, b_kmajor=False):
+    """C[M,N] = op(A) . op(B)^T with K split over workgroups and an fp32 workspace (mf_gemm_splitk):
+    for the weight gradients, few output tiles and K = tokens.  C fp16 or fp32."""
+    M, Ka = (A.shape[1], A.shape[0]) if a_kmajor else A.shape
+    N, Kb = (B.shape[1], B.shape[0]) if b_kmajor else B.shape
+    assert Ka == Kb, (A.shape, a_kmajor, B.shape, b_kmajor)
+    K = Ka
+    assert ws.dtype == torch.float32 and C.dtype in (torch.float16, torch.float32)
+    ev = None
+    if _PROBE is not None and _PROBE.wants("gemm"):
+        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), "gemm")
+    call("mf_gemm_splitk", _p(A), _ld(A), int(a_kmajor), _p(B), _ld(B), int(b_kmajor), _p(C), _ld(C), M, N, K,
+         _p(ws), ws.numel(), splits, int(C.dtype == torch.float16), _s())
+    if ev is not None:
+        ev.record()
+    return C
+
+
 def layernorm_fwd(x, gamma, beta, y=None, mean=None, rstd=None, row_index=None):
     rows = row_index.numel() if row_index is not None else x.shape[0]
     D = x.shape[1]

@@ -47,6 +47,15 @@ int mf_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, 
 int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb, int b_kmajor, void* C, int64_t ldc,
             int M, int N, int K, const void* bias, const void* aux_in, void* aux_out, int64_t ld_aux, int epilogue,
             int tile, void* stream);
+/* Split-K plain product (no epilogue) for few output tiles and a long K, e.g. the weight gradients
+ * dW = dY^T X with K = tokens (autograd's torch.mm(grad.t(), x) of nn.Linear, clip/model.py:274-280):
+ * `splits` 128x128-tile workgroups per tile each reduce a K slice into an fp32 plane of ws, then the
+ * planes are summed in a fixed order into C (fp16 if out_f16, else fp32).  splits <= 0: automatic.
+ * ws: mf_gemm_splitk_ws_floats(M, N, K, splits) floats.  Layout flags as mf_gemm; N % 8 == 0.     */
+int mf_gemm_splitk(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb, int b_kmajor, void* C,
+                   int64_t ldc, int M, int N, int K, float* ws, int64_t ws_floats, int splits, int out_f16,
+                   void* stream);
+int mf_gemm_splitk_ws_floats(int M, int N, int K, int splits);
 
 /* ---- LayerNorm (fp16 io, fp32 math; clip/model.py:153-159) --------------------------------
  * row_index (optional, int32): output row i normalises input row row_index[i]

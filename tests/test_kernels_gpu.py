@@ -80,6 +80,32 @@ def test_gemm_kmajor(dev, M, N, K, ak, bk, tile):
         assert torch.equal(C0, C32)
 
 
+
+@pytest.mark.parametrize("M,N,K,ak,bk,splits", [(3072, 768, 6368, True, True, 0), (768, 768, 6368, True, True, 0),
+                                                (2048, 512, 2926, True, True, 0), (256, 384, 1000, True, True, 3),
+                                                (512, 256, 4096, False, False, 0), (384, 512, 2048, True, False, 5)])
+def test_gemm_splitk(dev, M, N, K, ak, bk, splits):
+    """Split-K weight-gradient GEMM: fp32 partial planes summed in a fixed order -- against fp64, and
+    bit-reproducible run to run; one split equals the single-pass fp32 GEMM exactly."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = torch.randn(K, M, generator=g).half().to(dev) if ak else torch.randn(M, K, generator=g).half().to(dev)
+    B = ((torch.randn(K, N, generator=g) if bk else torch.randn(N, K, generator=g)) * K ** -0.5).half().to(dev)
+    ref = (A.double().t() if ak else A.double()) @ (B.double() if bk else B.double().t())
+    ws = torch.empty(ops.gemm_splitk_ws_floats(M, N, K, splits), device=dev)
+    C = torch.empty(M, N, device=dev, dtype=torch.float16)
+    ops.gemm_splitk(A, B, C, ws, splits=splits, a_kmajor=ak, b_kmajor=bk)
+    assert_ulps(C, ref, 1.0, 2e-2, "gemm splitk")
+    C32 = torch.empty(M, N, device=dev)
+    ops.gemm_splitk(A, B, C32, ws, splits=splits, a_kmajor=ak, b_kmajor=bk)
+    torch.testing.assert_close(C32.double(), ref, rtol=1e-5, atol=1e-4)
+    C32b = torch.empty_like(C32)
+    ops.gemm_splitk(A, B, C32b, ws, splits=splits, a_kmajor=ak, b_kmajor=bk)
+    assert torch.equal(C32, C32b)
+    one = torch.empty_like(C32)
+    ws1 = torch.empty(ops.gemm_splitk_ws_floats(M, N, K, 1), device=dev)
+    ops.gemm_splitk(A, B, one, ws1, splits=1, a_kmajor=ak, b_kmajor=bk)
+    assert torch.equal(one, ops.gemm(A, B, epilogue=ops.EPI_F32, tile=1, a_kmajor=ak, b_kmajor=bk))
+
 def test_gemm_kmajor_dgelu(dev):
     torch.manual_seed(5)
     M, N, K = 600, 1024, 256
