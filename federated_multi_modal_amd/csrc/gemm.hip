@@ -185,12 +185,13 @@ MF_DEV void epilogue_store(const GemmArgs& g, f16* lds, const f32x4 (&acc)[TM][T
     const int n = n0 + 8 * c8;
     const int cnt = min(8, g.N - n);
     const int r0 = tid / CPR;
+    const bool st_ok = r0 < RPP;  // CPR not dividing NT (BN = 192): the leftover threads store nothing
     // global operands first: residual / pre-activation rows of this thread's store passes, bias
     f16x8 auxv[NPASS];
 #pragma unroll
     for (int p = 0; p < NPASS; ++p) {
       const int m = m0 + r0 + p * RPP;
-      auxv[p] = (cnt > 0 && r0 + p * RPP < BM && m < g.M) ? epi_prefetch<EPI>(g, m, n, cnt) : f16x8{};
+      auxv[p] = (st_ok && cnt > 0 && r0 + p * RPP < BM && m < g.M) ? epi_prefetch<EPI>(g, m, n, cnt) : f16x8{};
     }
     f16x4 bv[TN];
 #pragma unroll
@@ -219,7 +220,7 @@ MF_DEV void epilogue_store(const GemmArgs& g, f16* lds, const f32x4 (&acc)[TM][T
       }
     }
     __syncthreads();
-    if (cnt > 0) {
+    if (st_ok && cnt > 0) {
 #pragma unroll
       for (int p = 0; p < NPASS; ++p) {
         const int r = r0 + p * RPP;
@@ -708,6 +709,10 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
     if (t256 >= 192 && t256 <= 256 && K >= 512)
       tile = 20;  // one round of 256x256 tiles on one workgroup per CU (vision QKV: 225 tiles)
+    else if (M >= 4096 && K >= 512)
+      tile = 10;  // 160x128: the vision N = 768 products as 240 tiles (one round), N = 3072 as 960;
+                  // +6..18 % over 128x64 / 128x128 on every vision shape (gemm_bench.py); text
+                  // (M = 2926) stays on 128-row tiles, where 160 rows measured slower
     else
       tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
   }
@@ -718,6 +723,10 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     case 4: return launch_tile<256, 128, 4, 2, 2>(a, epilogue, st);
     case 6: return launch_tile<128, 128, 2, 2, 3>(a, epilogue, st);
     case 7: return launch_tile<128, 64, 2, 2, 3>(a, epilogue, st);
+    case 8: return launch_tile<128, 192, 2, 2, 3>(a, epilogue, st);
+    case 9: return launch_tile<128, 192, 2, 2, 2>(a, epilogue, st);
+    case 10: return launch_tile<160, 128, 2, 2, 2>(a, epilogue, st);
+    case 11: return launch_tile<160, 128, 2, 2, 3>(a, epilogue, st);
     case 20: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 256, 2, 4>(a, epilogue, st);
     case 21: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 2, 4>(a, epilogue, st);
     case 22: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 4, 2>(a, epilogue, st);
