@@ -16,6 +16,7 @@
 // an L2.  The MFMA is issued "swapped" (weight fragment as the A operand) so each lane ends with
 // 4 consecutive output columns of one row -> 8-byte stores.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "mf_common.h"
@@ -647,6 +648,12 @@ int launch_kmajor(const GemmArgs& a, bool ta, bool tb, int epi, int tile, hipStr
 #undef MF_KM
 }
 
+// tile-rule A/B knob (MAPFED_GEMM_RULE=1: every vision product on 160x128, text on 128-row tiles)
+inline int gemm_rule() {
+  static const int r = getenv("MAPFED_GEMM_RULE") ? atoi(getenv("MAPFED_GEMM_RULE")) : 0;
+  return r;
+}
+
 // automatic split count (tests/diagnostics/splitk_bench.py on the MaPLe dW shapes, K = 2926..6368):
 // >= 144 128x128 tiles run best unsplit; 64..143 tiles on 4 slices; fewer on 8
 inline int splitk_auto(int64_t tiles) { return tiles >= 144 ? 1 : (tiles >= 64 ? 4 : 8); }
@@ -709,10 +716,12 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
     if (t256 >= 192 && t256 <= 256 && K >= 512)
       tile = 20;  // one round of 256x256 tiles on one workgroup per CU (vision QKV: 225 tiles)
-    else if (M >= 4096 && K >= 512)
-      tile = 10;  // 160x128: the vision N = 768 products as 240 tiles (one round), N = 3072 as 960;
-                  // +6..18 % over 128x64 / 128x128 on every vision shape (gemm_bench.py); text
-                  // (M = 2926) stays on 128-row tiles, where 160 rows measured slower
+    else if (M >= 4096 && K >= 512)  // vision products (M = 6368), tests/diagnostics/gemm_bench.py:
+      // N = 3072: 160x128 (960 tiles); N = 768: 96x128 (402 tiles, two workgroups per CU) for K >= 2048,
+      // 160x64 (480 tiles) for K = 768; +6..37 % over the 128-row tiles
+      tile = (N > 1024 || gemm_rule() == 1) ? 10 : (K >= 2048 ? 15 : 16);
+    else if (M >= 2048 && N >= 1024 && K <= 768 && gemm_rule() != 1)
+      tile = 26;  // text QKV / c_fc (M = 2926): 96x64
     else
       tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
   }
@@ -727,6 +736,17 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     case 9: return launch_tile<128, 192, 2, 2, 2>(a, epilogue, st);
     case 10: return launch_tile<160, 128, 2, 2, 2>(a, epilogue, st);
     case 11: return launch_tile<160, 128, 2, 2, 3>(a, epilogue, st);
+    case 12: return launch_tile<192, 128, 2, 2, 2>(a, epilogue, st);
+    case 13: return launch_tile<128, 160, 2, 2, 2>(a, epilogue, st);
+    case 14: return launch_tile<160, 160, 2, 2, 2>(a, epilogue, st);
+    case 15: return launch_tile<96, 128, 2, 2, 2>(a, epilogue, st);
+    case 16: return launch_tile<160, 64, 2, 2, 2>(a, epilogue, st);
+    case 17: return launch_tile<224, 128, 2, 2, 2>(a, epilogue, st);
+    case 18: return launch_tile<96, 128, 2, 2, 3>(a, epilogue, st);
+    case 19: return launch_tile<128, 96, 2, 2, 2>(a, epilogue, st);
+    case 25: return launch_tile<96, 192, 2, 2, 2>(a, epilogue, st);
+    case 26: return launch_tile<96, 64, 2, 2, 2>(a, epilogue, st);
+    case 27: return launch_tile<64, 128, 2, 2, 2>(a, epilogue, st);
     case 20: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 256, 2, 4>(a, epilogue, st);
     case 21: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 2, 4>(a, epilogue, st);
     case 22: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 4, 2>(a, epilogue, st);

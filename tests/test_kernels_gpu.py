@@ -41,7 +41,10 @@ def assert_ulps(out, ref, max_ulp=1.0, frac=1e-2, what="", floor=2e-5):
                                         (131, 388, 192, 9),
                                         # 160x128 (tiles 10, 11)
                                         (6368, 768, 3072, 10), (333, 136, 128, 10), (6368, 768, 2304, 11),
-                                        (170, 260, 192, 11)])
+                                        (170, 260, 192, 11),
+                                        # 96x128, 160x64, 96x64 (tiles 15, 16, 26) as chosen by the heuristic
+                                        (6368, 768, 3072, 0), (6368, 768, 768, 0), (2926, 1536, 512, 0),
+                                        (97, 200, 64, 15), (161, 72, 128, 16), (100, 76, 192, 26)])
 def test_gemm_bias(dev, M, N, K, tile):
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g).half().to(dev)
