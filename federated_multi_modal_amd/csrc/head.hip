@@ -47,7 +47,7 @@ __global__ void logits_kernel(const f16* __restrict__ img_n, const f16* __restri
   }
 }
 
-// Single block of 256 threads (4 waves); wave w handles rows b = w, w+4, ...
+// Single block of 1024 threads (16 waves); wave w handles rows b = w, w+16, ...
 // out: loss_out[0] = total (fp16 value as fp32), [1] = CE, [2] = alignment, [3] = nonfinite flag
 // dmm[b,k] = fp16(fp16((softmax - onehot)/B) * scale);  cosg[b] = d cos[b] = fp16(-0.5/B)
 // cos needs u = fp16(img_n/||img_n||16), v = fp16(t/||t||16) (cosine_similarity normalises again)
@@ -56,9 +56,9 @@ __global__ void loss_kernel(const f16* __restrict__ logits, const f16* __restric
                             const float* __restrict__ logit_scale, f16* __restrict__ dmm,
                             float* __restrict__ cos_out, float* __restrict__ loss_out) {
   __shared__ float s_ce[64], s_cos[64];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const float sc = fminf(expf(logit_scale[0]), 100.f);
-  for (int b = w; b < B; b += 4) {
+  for (int b = w; b < B; b += nw) {
     const f16* lr = logits + (int64_t)b * K;
     const int y = (int)label[b];
     float mx = -INFINITY;
@@ -201,7 +201,7 @@ __global__ void soft_target_kernel(const float* __restrict__ q, const f16* __res
   }
 }
 
-// Single block of 256 threads, wave w handles rows b = w, w+4, ...
+// Single block of 1024 threads, wave w handles rows b = w, w+16, ...
 //   log_probs = fp16(log_softmax(logits)); t = max(q, 1e-8)
 //   KL = sum_{b,k} t (log t - log_probs) / B  in fp32 (F.kl_div(..., "batchmean") of an fp16 input and an
 //   fp32 target promotes to fp32); its input gradient fp16(-t/B) goes through the log_softmax backward:
@@ -213,11 +213,11 @@ __global__ void loss_soft_kernel(const f16* __restrict__ logits, const f16* __re
                                  const float* __restrict__ logit_scale, f16* __restrict__ dmm,
                                  f16* __restrict__ gtgt, float* __restrict__ cos_out, float* __restrict__ loss_out) {
   __shared__ float s_kl[64], s_cos[64];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const float sc = fminf(expf(logit_scale[0]), 100.f);
   const float invB = 1.0f / (float)B;
   const float dcos = r16(-0.5f * invB);
-  for (int b = w; b < B; b += 4) {
+  for (int b = w; b < B; b += nw) {
     const f16* lr = logits + (int64_t)b * K;
     const float* qr = q + (int64_t)b * K;
     float mx = -INFINITY;
@@ -400,7 +400,7 @@ extern "C" int mf_clip_loss_fwd_bwd(const void* img, const void* txt, const void
                                     void* dimg_n, void* dtxt_n, void* dimg, void* dtxt, void* stream) {
   if (B > 64) return mf_set_error("mf_clip_loss_fwd_bwd: B <= 64", -1);
   hipStream_t st = (hipStream_t)stream;
-  loss_kernel<<<1, 256, 0, st>>>((const f16*)logits, (const f16*)img_n, (const f16*)txt_n, label, B, K, D,
+  loss_kernel<<<1, 1024, 0, st>>>((const f16*)logits, (const f16*)img_n, (const f16*)txt_n, label, B, K, D,
                                  logit_scale, (f16*)dmm, cos_ws, loss_out);
   dimg_kernel<<<B, 256, 0, st>>>((const f16*)dmm, (const f16*)img_n, (const f16*)txt_n, label, nullptr, cos_ws, B,
                                  K, D, (f16*)dimg_n);
@@ -423,7 +423,7 @@ extern "C" int mf_clip_loss_soft_fwd_bwd(const void* img, const void* txt, const
   f16* tgt = (f16*)soft_ws;
   f16* gtgt = tgt + (int64_t)B * D;
   soft_target_kernel<<<B, 256, 0, st>>>(label_probs, (const f16*)txt_n, K, D, tgt);
-  loss_soft_kernel<<<1, 256, 0, st>>>((const f16*)logits, (const f16*)img_n, tgt, label_probs, B, K, D, logit_scale,
+  loss_soft_kernel<<<1, 1024, 0, st>>>((const f16*)logits, (const f16*)img_n, tgt, label_probs, B, K, D, logit_scale,
                                       (f16*)dmm, gtgt, cos_ws, loss_out);
   dimg_kernel<<<B, 256, 0, st>>>((const f16*)dmm, (const f16*)img_n, (const f16*)txt_n, nullptr, tgt, cos_ws, B, K, D,
                                  (f16*)dimg_n);

@@ -184,7 +184,9 @@ __global__ __launch_bounds__(256) void ln_fwd2_kernel(const f16* __restrict__ x,
                                                      const int* __restrict__ ridx, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, f16* __restrict__ y,
                                                      int64_t ldy, float* __restrict__ mean_out,
-                                                     float* __restrict__ rstd_out, int rows) {
+                                                     float* __restrict__ rstd_out, int rows,
+                                                     const float* __restrict__ inj = nullptr, int inj_L = 1,
+                                                     int inj_row0 = 0, int inj_n = 0) {
   constexpr int CH = D / 256;  // 16-byte chunks per lane
   const int hl = threadIdx.x & 31;
   const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
@@ -193,8 +195,23 @@ __global__ __launch_bounds__(256) void ln_fwd2_kernel(const f16* __restrict__ x,
   const f16* xr = x + (int64_t)src * ldx;
   float v[CH * 8];
   f16x8 t[CH];
+  // deep-prompt injection fused in (inj != null, no ridx): rows inj_row0 .. inj_row0+inj_n-1 of every
+  // inj_L-row sequence take fp16(prompt row) -- written back to x as mf_prompt_inject_fwd would -- and
+  // are normalised from those values
+  const int pr = inj ? row % inj_L - inj_row0 : -1;
+  if (pr >= 0 && pr < inj_n) {
+    const float* prow = inj + (int64_t)pr * D;
 #pragma unroll
-  for (int j = 0; j < CH; ++j) t[j] = *(const f16x8*)(xr + 8 * (hl + 32 * j));
+    for (int j = 0; j < CH; ++j) {
+      const int c = 8 * (hl + 32 * j);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[j][e] = (f16)prow[c + e];
+      *(f16x8*)(const_cast<f16*>(xr) + c) = t[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < CH; ++j) t[j] = *(const f16x8*)(xr + 8 * (hl + 32 * j));
+  }
   // Reduction order identical to ln_fwd_kernel's: a 16-byte chunk holds the 4-element groups of two
   // of its lanes (2*hl and 2*hl+1); keep them as two partials, butterfly each over the half-wave
   // (= that kernel's xor 32..2 steps) and add them last (= its xor-1 step).
@@ -464,6 +481,34 @@ extern "C" int mf_col_reduce_batch(const void* descs, int n, int max_cols, void*
   if (n <= 0) return 0;
   col_reduce_batch_kernel<<<dim3((max_cols + 63) / 64, n), 1024, 0, (hipStream_t)stream>>>(
       (const ColReduceDesc*)descs);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_prompt_inject_fwd(void* x, const float* prompt, int N, int L, int row0, int nrows, int D,
+                                    void* stream);
+
+// LayerNorm with the deep-prompt injection of the same rows fused in: equivalent (bit for bit) to
+// mf_prompt_inject_fwd(x, prompt, rows / L, L, row0, nrows, D) followed by mf_layernorm_fwd on x
+// (clip/model.py:320-349 injection at the start of a block, then its ln_1).
+extern "C" int mf_layernorm_fwd_inject(void* x, int64_t ldx, const float* gamma, const float* beta, void* y,
+                                       int64_t ldy, float* mean, float* rstd, int rows, int D, const float* prompt,
+                                       int L, int row0, int nrows, void* stream) {
+  if (rows <= 0) return 0;
+  if (L <= 0 || rows % L || row0 < 0 || row0 + nrows > L) return mf_set_error("mf_layernorm_fwd_inject: rows", -1);
+  hipStream_t st = (hipStream_t)stream;
+  const bool v16 = ((uintptr_t)x % 16 == 0) && ((uintptr_t)y % 16 == 0) && (ldx % 8 == 0) && (ldy % 8 == 0);
+  if (ldx != D || !(ln_variant() == 2 && v16 && (D == 768 || D == 512))) {
+    const int rc = mf_prompt_inject_fwd(x, prompt, rows / L, L, row0, nrows, D, stream);
+    return rc ? rc : mf_layernorm_fwd(x, ldx, nullptr, gamma, beta, y, ldy, mean, rstd, rows, D, stream);
+  }
+  const dim3 g2((rows + 7) / 8);
+  if (D == 768)
+    ln_fwd2_kernel<768><<<g2, 256, 0, st>>>((const f16*)x, ldx, nullptr, gamma, beta, (f16*)y, ldy, mean, rstd, rows,
+                                            prompt, L, row0, nrows);
+  else
+    ln_fwd2_kernel<512><<<g2, 256, 0, st>>>((const f16*)x, ldx, nullptr, gamma, beta, (f16*)y, ldy, mean, rstd, rows,
+                                            prompt, L, row0, nrows);
   MF_CHECK_LAUNCH();
   return 0;
 }

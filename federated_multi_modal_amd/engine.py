@@ -210,10 +210,13 @@ class _Tower:
         N, L, D, H = self.N, self.L, self.D, self.H
         for i in range(self.layers):
             x = self.X[i]
-            if 1 <= i <= len(deep_prompts):
-                ops.prompt_inject_fwd(x, deep_prompts[i - 1], N, L, self.row0, N_CTX, D)
             h1 = self.H1
-            ops.layernorm_fwd(x, self.p(i, "ln_1.weight"), self.p(i, "ln_1.bias"), h1, self.mean1[i], self.rstd1[i])
+            if 1 <= i <= len(deep_prompts):  # deep prompts injected into x and ln_1 in one pass
+                ops.layernorm_fwd_inject(x, self.p(i, "ln_1.weight"), self.p(i, "ln_1.bias"), h1, self.mean1[i],
+                                         self.rstd1[i], deep_prompts[i - 1], L, self.row0, N_CTX)
+            else:
+                ops.layernorm_fwd(x, self.p(i, "ln_1.weight"), self.p(i, "ln_1.bias"), h1, self.mean1[i],
+                                  self.rstd1[i])
             ops.gemm_nt(h1, self.p(i, "attn.in_proj_weight"), self.QKV[i], bias=self.p(i, "attn.in_proj_bias"),
                         epilogue=ops.EPI_BIAS)
             ops.attention_fwd(self.QKV[i], N, L, H, self.causal, out=self.O[i], lse=self.LSE[i])

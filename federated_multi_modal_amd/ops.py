@@ -155,6 +155,15 @@ def layernorm_fwd(x, gamma, beta, y=None, mean=None, rstd=None, row_index=None):
     return y, mean, rstd
 
 
+
+def layernorm_fwd_inject(x, gamma, beta, y, mean, rstd, prompt, L, row0, nrows):
+    """prompt_inject_fwd(x, prompt, ...) + layernorm_fwd(x, ...) in one kernel (bit-identical)."""
+    rows, D = x.shape
+    call("mf_layernorm_fwd_inject", _p(x), _ld(x), _p(gamma), _p(beta), _p(y), _ld(y), _p(mean), _p(rstd), rows, D,
+         _p(prompt), L, row0, nrows, _s())
+    return y, mean, rstd
+
+
 def layernorm_ws_floats(rows: int, D: int) -> int:
     return 2 * call("mf_layernorm_bwd_blocks", rows) * D
 

@@ -62,6 +62,12 @@ int mf_gemm_splitk_ws_floats(int M, int N, int K, int splits);
  * (ln_post on class tokens clip/model.py:567, ln_final + EOT gather trainers/maple.py:72-76).    */
 int mf_layernorm_fwd(const void* x, int64_t ldx, const int* row_index, const float* gamma, const float* beta,
                      void* y, int64_t ldy, float* mean, float* rstd, int rows, int D, void* stream);
+/* mf_prompt_inject_fwd(x, prompt, rows / L, L, row0, nrows, D) then mf_layernorm_fwd(x, ...), in one
+ * pass (bit-identical): the deep prompts injected at the start of a block and that block's ln_1
+ * (clip/model.py:320-349, 153-159).  x is written (the injected rows).                            */
+int mf_layernorm_fwd_inject(void* x, int64_t ldx, const float* gamma, const float* beta, void* y, int64_t ldy,
+                            float* mean, float* rstd, int rows, int D, const float* prompt, int L, int row0,
+                            int nrows, void* stream);
 /* dx = fp16(dres + fp16(LN'(dy)))  (dres optional; dx may alias dres); dgamma/dbeta written or
  * accumulated (accumulate != 0).  workspace: 2 * mf_layernorm_bwd_blocks(rows) * D floats.        */
 int mf_layernorm_bwd_blocks(int rows);

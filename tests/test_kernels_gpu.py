@@ -552,3 +552,20 @@ def test_argmax_correct(dev):
     ref = logits.float().cpu().argmax(1)
     assert torch.equal(pred.cpu(), ref)
     assert acc[0].item() == (ref == label.cpu()).sum().item() and acc[1].item() == B
+
+
+@pytest.mark.parametrize("N,L,D,row0", [(5, 199, 768, 197), (7, 77, 512, 1)])
+def test_layernorm_fwd_inject_equals_inject_then_ln(dev, N, L, D, row0):
+    """The fused deep-prompt injection + ln_1 is bit-identical to the two separate kernels."""
+    torch.manual_seed(L)
+    x = torch.randn(N * L, D).half().to(dev)
+    prompt = torch.randn(2, D).to(dev)
+    g, b = torch.randn(D).to(dev), torch.randn(D).to(dev)
+    x1 = x.clone()
+    ops.prompt_inject_fwd(x1, prompt, N, L, row0, 2, D)
+    y1, m1, r1 = ops.layernorm_fwd(x1, g, b)
+    x2 = x.clone()
+    y2 = torch.empty_like(y1)
+    m2, r2 = torch.empty_like(m1), torch.empty_like(r1)
+    ops.layernorm_fwd_inject(x2, g, b, y2, m2, r2, prompt, L, row0, 2)
+    assert torch.equal(x1, x2) and torch.equal(y1, y2) and torch.equal(m1, m2) and torch.equal(r1, r2)
