@@ -105,9 +105,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("MAPFED_DIST_BACKEND", "nccl") != "nccl":
+        local %= max(torch.cuda.device_count(), 1)  # rehearsal: ranks share the box's GPU(s)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # MAPFED_DIST_BACKEND=gloo: rehearse the multi-rank path with several ranks on one GPU (RCCL refuses
+        # two ranks on one device); the driver's runs use RCCL, one rank per GPU
+        backend = os.environ.get("MAPFED_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     J, K, B, desc = CONFIGS[args.config]

@@ -245,6 +245,9 @@ class MaPLe(TrainerX):
         loss = float(self._loss_sum.item()) - before
         if self.engine.loss_out[3].item() != 0.0:
             raise RuntimeError("NaN/Inf in total loss")
+        # the grad-norm log of trainers/maple.py:605-612 (norm of the clipped gradients): total * coef
+        total, coef = self.engine.clip_out[:2].tolist()
+        self.grad_norms.append(total * coef)
         return {"loss": loss}
 
     def run_epoch(self, epoch):

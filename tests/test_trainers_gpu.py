@@ -30,6 +30,7 @@ def test_federated_round_checkpoint_and_eval_only(dev, tmp_path):
     assert len(tr.clients) == 2 and tr.clients[0].engine.K == 10
     res = tr.clients[0].forward_backward(next(iter(tr.clients[0].dm.train_loader)))
     assert isinstance(res["loss"], float) and res["loss"] == res["loss"]
+    assert len(tr.clients[0].grad_norms) == 1 and 0.0 < tr.clients[0].grad_norms[0] <= 1.0 + 1e-3
     # FedAvg of two clients == the reference's safe_average_weights on their trainables (bit-exact)
     for c in tr.clients:
         c.run_epoch(0)
