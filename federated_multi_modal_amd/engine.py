@@ -184,6 +184,8 @@ class _Tower:
         self.dQKV = e(R, 3 * D)
         self.dF = e(R, 4 * D)
         self.attn_ws = e(N * H * L, dt=F32)
+        # this tower's LayerNorm dgamma/dbeta partials, reduced in one launch at the end of its backward
+        self.lnb = ops.LNGradBatch(dev)
         self.cs_ws = e(ops.colsum_ws_floats(R, 4 * D), dt=F32)
         # split-K weight gradients of the trainable block (few output tiles, K = R tokens): fp32 partial
         # planes, summed in a fixed order (MAPFED_DW_SPLITK=0: the single-pass K-major GEMM)
@@ -254,7 +256,7 @@ class _Tower:
             ops.gemm_nt(self.dF, self.wt(i, "mlp.c_fc.weight"), self.dH, epilogue=ops.EPI_NONE)
             if trainable_w:
                 self._dw(self.dF, self.H2, self.g(i, "mlp.c_fc.weight"), self.g(i, "mlp.c_fc.bias"))
-            self.e.lnb.bwd(self.dH, self.X1[i], self.p(i, "ln_2.weight"), self.mean2[i], self.rstd2[i], dX,
+            self.lnb.bwd(self.dH, self.X1[i], self.p(i, "ln_2.weight"), self.mean2[i], self.rstd2[i], dX,
                            self.g(i, "ln_2.weight"), self.g(i, "ln_2.bias"), dres=dX)
             # ---- attention: X1 = X + out_proj(attn(ln_1(X)))
             ops.gemm_nt(dX, self.wt(i, "attn.out_proj.weight"), self.dO, epilogue=ops.EPI_NONE)
@@ -265,7 +267,7 @@ class _Tower:
             ops.gemm_nt(self.dQKV, self.wt(i, "attn.in_proj_weight"), self.dH, epilogue=ops.EPI_NONE)
             if trainable_w:
                 self._dw(self.dQKV, self.H1, self.g(i, "attn.in_proj_weight"), self.g(i, "attn.in_proj_bias"))
-            self.e.lnb.bwd(self.dH, self.X[i], self.p(i, "ln_1.weight"), self.mean1[i], self.rstd1[i], dX,
+            self.lnb.bwd(self.dH, self.X[i], self.p(i, "ln_1.weight"), self.mean1[i], self.rstd1[i], dX,
                            self.g(i, "ln_1.weight"), self.g(i, "ln_1.bias"), dres=dX)
             if 1 <= i <= n_prompted:
                 ops.prompt_inject_bwd(dX, N, L, self.row0, N_CTX, D, prompt_grads[i - 1], accumulate=False,
@@ -308,7 +310,6 @@ class MapleEngine:
                           True, 1)
         self._build_io()
         self.side = torch.cuda.Stream(device=self.device)
-        self.lnb = ops.LNGradBatch(self.device)
         self.overlap_towers = True  # False: both towers on the current stream (isolated kernel timing)
         self.step_count = 0
         self.momentum_initialised = False
@@ -594,31 +595,40 @@ class MapleEngine:
         t = self.txt
         ops.gemm_nt(self.dtxt, P["text_encoder.text_projection"], self.d_txt_final, epilogue=ops.EPI_NONE)
         t.dX.zero_()
-        self.lnb.bwd(self.d_txt_final, t.X[-1], P["text_encoder.ln_final.weight"], self.fin_mean, self.fin_rstd,
+        t.lnb.bwd(self.d_txt_final, t.X[-1], P["text_encoder.ln_final.weight"], self.fin_mean, self.fin_rstd,
                      t.dX, G["text_encoder.ln_final.weight"], G["text_encoder.ln_final.bias"],
                           row_index=self.eot_rows)
         t.backward(self.J - 1, self.g_txt_deep)
         # d ctx (text path): sum over classes of the rows 1..n_ctx of d prompts (fp16 result)
         ops.prompt_inject_bwd(t.dX, self.K, t.L, 1, N_CTX, t.D, self.G["prompt_learner.ctx"], accumulate=False,
                               zero_rows=False)
+        t.lnb.finish()  # the text LayerNorms' dgamma/dbeta, on the text stream (overlaps the vision backward)
 
     def _vision_backward(self):
         P, G = self.P, self.G
         v = self.vis
         ops.gemm_nt(self.dimg, P["image_encoder.proj"], self.d_vis_post, epilogue=ops.EPI_NONE)
         v.dX.zero_()
-        self.lnb.bwd(self.d_vis_post, v.X[-1], P["image_encoder.ln_post.weight"], self.post_mean,
+        v.lnb.bwd(self.d_vis_post, v.X[-1], P["image_encoder.ln_post.weight"], self.post_mean,
                           self.post_rstd, v.dX, G["image_encoder.ln_post.weight"], G["image_encoder.ln_post.bias"],
                      row_index=self.cls_rows)
         v.backward(self.J - 1, self.g_vis_deep)
-        self.lnb.bwd(v.dX, self.Xpre, P["image_encoder.ln_pre.weight"], self.pre_mean, self.pre_rstd, self.dXpre,
+        v.lnb.bwd(v.dX, self.Xpre, P["image_encoder.ln_pre.weight"], self.pre_mean, self.pre_rstd, self.dXpre,
                      G["image_encoder.ln_pre.weight"], G["image_encoder.ln_pre.bias"])
         ops.prompt_inject_bwd(self.dXpre, self.B, self.Lv, self.G2 + 1, N_CTX, v.D, self.g_shared_ctx,
                               accumulate=False, zero_rows=False)
+        v.lnb.finish()
 
     def forward_backward(self):
-        """loss = CustomCLIP(image, label); loss.backward()  — grads land in gflat16/gflat32."""
-        self.forward()
+        """loss = CustomCLIP(image, label); loss.backward()  — grads land in gflat16/gflat32.
+        The trainable block's W^T copies (read by its dX products) are refreshed from the current
+        weights first, on the side stream, where they overlap the vision forward."""
+        main = torch.cuda.current_stream(self.device)
+        side = self.side if self.overlap_towers else main
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self.refresh_transposes(all_layers=False)
+        self.forward()  # joins the side stream before returning
         if self.soft_labels:
             ops.clip_loss_soft_fwd_bwd(self.img_feat, self.txt_feat, self.img_n, self.txt_n, self.norms,
                                        self.logits, self.soft_label_in, self.P["logit_scale"], self.dmm, self.cos_ws,
@@ -634,7 +644,6 @@ class MapleEngine:
             self._text_backward()
         self._vision_backward()
         main.wait_stream(side)
-        self.lnb.finish()  # every LayerNorm's dgamma/dbeta in one reduction launch
         self._prompt_learner_bwd()
 
     # ------------------------------------------------------------------ optimizer
@@ -652,7 +661,6 @@ class MapleEngine:
         ops.sgd_step(self.flat16, self.gflat16, self.mom16, self.clip_out, self.hyper)
         ops.sgd_step(self.flat32, self.gflat32, self.mom32, self.clip_out, self.hyper)
         self.hyper[3:4].zero_()  # a device fill, legal inside graph capture
-        self.refresh_transposes(all_layers=False)
 
     def train_step(self):
         self.forward_backward()
