@@ -12,7 +12,7 @@ import sys
 from collections import defaultdict
 
 FAMILIES = [("gemm", "gemm"), ("attention", "attn_"), ("layernorm", "ln_"), ("transpose", "transpose"),
-            ("optim", "sgd_kernel")]
+            ("optim", "sgd")]
 
 
 def family(name):

@@ -18,7 +18,7 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     idx = int(sys.argv[2]) if len(sys.argv) > 2 else -3
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Queue_Id"], r["Kernel_Name"]) for r in rows))
-    ends = [i for i, k in enumerate(ks) if "sgd_kernel" in k[3]]
+    ends = [i for i, k in enumerate(ks) if re.search(r"sgd8?_kernel", k[3])]
     # a step = kernels after the previous step's sgd (exclusive) .. this step's last sgd (inclusive)
     groups, prev = [], -1
     for i in ends:
