@@ -721,7 +721,7 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
       // 160x64 (480 tiles) for K = 768; +6..37 % over the 128-row tiles
       tile = (N > 1024 || gemm_rule() == 1) ? 10 : (K >= 2048 ? 15 : 16);
     else if (M >= 2048 && N >= 1024 && K <= 768 && gemm_rule() != 1)
-      tile = 26;  // text QKV / c_fc (M = 2926): 96x64
+      tile = N >= 2048 ? 15 : 26;  // text (M = 2926): c_fc and its dX on 96x128, QKV on 96x64
     else
       tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
   }
