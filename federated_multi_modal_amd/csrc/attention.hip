@@ -642,7 +642,7 @@ MF_DEV void fwd4_tile(const f16* sK, const f16* sV, const int* koff, const int* 
 // scores start once Q and K have landed (vmcnt = this wave's V loads) and V is waited for only before
 // P.V, so the V transfer runs under the score MFMAs and the softmax.
 template <int LKP, bool CAUSAL>
-__global__ __launch_bounds__(512, 4) void attn_fwd4_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
+__global__ __launch_bounds__(1024) void attn_fwd4_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
                                                            f16* __restrict__ out, int64_t ld_out,
                                                            float* __restrict__ lse, int ld_lse, int L, int H) {
   __shared__ __attribute__((aligned(16))) f16 sK[LKP * 64];
@@ -1124,7 +1124,7 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
   if (fwd_variant == 4) {
     // the head's 16-query tiles split evenly over its workgroups (no workgroup without a tile)
     const int qs4 = attn_qsplit(N * H, L), tiles = (L + 15) / 16;
-    const dim3 grid4(N * H, qs4), block4(64 * std::min(8, (tiles + qs4 - 1) / qs4));
+    const dim3 grid4(N * H, qs4), block4(64 * std::min(16, (tiles + qs4 - 1) / qs4));
     const int LP16 = tiles * 16;  // keys staged in 16-row tiles (LP16 % 32 == 16: a half last chunk)
 #define CALLF4(P)                                                                                             \
   if (causal)                                                                                                 \
