@@ -234,3 +234,38 @@ def test_eot_truncated_text_tower_matches_full(dev):
     worst = max(((g1[n] - g0[n]).norm() / (g0[n].norm() + 1e-30)).item() for n in g0)
     print(f"text_len {lt}: worst grad rel diff {worst:.2e}")
     assert worst <= 1e-2
+
+
+def test_c4_full_size_properties(dev):
+    """BASELINE configs[3] size (B=32, K=38, J=9), where the oracle is too slow to run: size-independent
+    properties.  Two engines from one seed agree bit for bit (logits, loss, every gradient, the updated
+    weights); the EOT-truncated text tower gives bit-identical logits and loss; cached-text eval equals a
+    full forward; everything finite."""
+    J, K, B, seed = 9, 38, 32, 0
+    names = syn.synthetic_classnames(K, seed)
+    b = syn.client_batch(seed, 0, 0, B, K)
+    runs = []
+    for trunc in (False, False, True):
+        e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed, eot_truncate=trunc),
+                        device=dev)
+        e.set_lr(0.0026)
+        e.load_batch(torch.from_numpy(b.images), torch.from_numpy(b.labels))
+        logits = e.forward().clone()
+        e.forward_backward()
+        loss = e.loss()
+        grads = {k: v.detach().clone() for k, v in e.grads().items()}
+        e.optimizer_step()
+        params = {k: v.detach().clone() for k, v in e.trainable_state().items()}
+        runs.append((logits, loss, grads, params, e))
+    (l0, s0, g0, p0, e0), (l1, s1, g1, p1, _), (l2, s2, _, _, _) = runs
+    assert torch.isfinite(l0.float()).all() and np.isfinite(s0)
+    assert torch.equal(l0, l1) and s0 == s1
+    assert all(torch.equal(g0[k], g1[k]) for k in g0) and all(torch.equal(p0[k], p1[k]) for k in p0)
+    assert all(torch.isfinite(v.float()).all() for v in g0.values())
+    assert torch.equal(l0, l2) and s0 == s2
+    # eval with the text features of the previous forward (weights updated since: re-encode once first)
+    full = e0.forward().clone()
+    e0.load_batch(torch.from_numpy(syn.client_batch(seed, 0, 1, B, K).images))
+    full2 = e0.forward().clone()
+    cached2 = e0.forward(reuse_text=True).clone()
+    assert torch.equal(full2, cached2) and not torch.equal(full, full2)
