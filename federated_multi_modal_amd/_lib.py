@@ -42,6 +42,7 @@ SIGNATURES = {
     "mf_small_linear_bwd_batch": [P, I, I, I, I, P],
     "mf_clip_head_fwd": [P, P, I, I, I, P, P, P, P, P, P, P],
     "mf_clip_loss_fwd_bwd": [P, P, P, P, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P],
+    "mf_layernorm_bwd_inject": [P, L, P, L, P, P, P, P, L, P, L, P, I, I, P, I, I, I, P],
     "mf_layernorm_fwd_inject": [P, L, P, P, P, L, P, P, I, I, P, I, I, I, P],
     "mf_gemm_splitk": [P, L, I, P, L, I, P, L, I, I, I, P, L, I, I, P],
     "mf_clip_loss_soft_fwd_bwd": [P, P, P, P, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P],

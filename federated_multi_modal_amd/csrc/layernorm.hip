@@ -268,7 +268,8 @@ __global__ __launch_bounds__(256) void ln_bwd2_kernel(const f16* __restrict__ dy
                                                      const float* __restrict__ rstd_in, const f16* dres,
                                                      int64_t ldres, f16* dx, int64_t lddx,
                                                      float* __restrict__ dg_part, float* __restrict__ db_part,
-                                                     int rows) {
+                                                     int rows, float* __restrict__ inj_part = nullptr,
+                                                     int inj_L = 1, int inj_row0 = 0, int inj_n = 0) {
   constexpr int CH = D / 256;
   constexpr int RPH = LN_ROWS_PER_BLOCK / 8;  // rows per half-wave
   __shared__ float red_g[8][D];
@@ -335,6 +336,11 @@ __global__ __launch_bounds__(256) void ln_bwd2_kernel(const f16* __restrict__ dy
       const float b = (sdg * mean - sdgx) * rstd * rstd * rstd * invD;
       const float c = -b * mean - sdg * rstd * invD;
       f16* dxr = dx + (int64_t)srcs[k] * lddx;
+      // injected deep-prompt rows (inj_part != null, no ridx): their gradient goes to the prompt, not to
+      // the previous layer -- the fp16 value is kept as an fp32 partial [sequence][prompt row][D] (summed
+      // over sequences by the deferred column reduction) and the dx row is zeroed
+      const int pr = inj_part ? srcs[k] % inj_L - inj_row0 : -1;
+      float* ipr = (pr >= 0 && pr < inj_n) ? inj_part + ((int64_t)(srcs[k] / inj_L) * inj_n + pr) * D : nullptr;
 #pragma unroll
       for (int j = 0; j < CH; ++j) {
         f16x8 o;
@@ -343,6 +349,12 @@ __global__ __launch_bounds__(256) void ln_bwd2_kernel(const f16* __restrict__ dy
           const float t = ((rstd * (float)td[k][j][e]) * gv[j * 8 + e] + b * (float)tx[k][j][e]) + c;
           const float t16 = r16(t);
           o[e] = dres ? (f16)((float)tr[k][j][e] + t16) : (f16)t16;
+        }
+        if (ipr) {
+          const int cc = 8 * (hl + 32 * j);
+          *(f32x4*)(ipr + cc) = (f32x4){(float)o[0], (float)o[1], (float)o[2], (float)o[3]};
+          *(f32x4*)(ipr + cc + 4) = (f32x4){(float)o[4], (float)o[5], (float)o[6], (float)o[7]};
+          o = f16x8{};
         }
         *(f16x8*)(dxr + 8 * (hl + 32 * j)) = o;
       }
@@ -509,6 +521,38 @@ extern "C" int mf_layernorm_fwd_inject(void* x, int64_t ldx, const float* gamma,
   else
     ln_fwd2_kernel<512><<<g2, 256, 0, st>>>((const f16*)x, ldx, nullptr, gamma, beta, (f16*)y, ldy, mean, rstd, rows,
                                             prompt, L, row0, nrows);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+// LayerNorm backward (partials only, as mf_layernorm_bwd with dgamma = dbeta = NULL) with the deep-prompt
+// injection backward of the same rows fused in: rows row0 .. row0+nrows-1 of every L-row sequence
+// write their dx value as an fp32 partial inj_part[n][r][D] (the prompt gradient is their sum over n,
+// left to the caller's mf_col_reduce_batch with nblk = rows / L, C = nrows * D) and a zero dx row.
+// Replaces mf_layernorm_bwd + mf_prompt_inject_bwd(zero_rows) (clip/model.py:153-159, 320-349).
+extern "C" int mf_layernorm_bwd_inject(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* gamma,
+                                       const float* mean, const float* rstd, const void* dres, int64_t ldres,
+                                       void* dx, int64_t lddx, float* workspace, int rows, int D, float* inj_part,
+                                       int L, int row0, int nrows, void* stream) {
+  if (rows <= 0) return 0;
+  if (D != 512 && D != 768) return mf_set_error("mf_layernorm_bwd_inject: D must be 512 or 768", -1);
+  if (L <= 0 || rows % L || row0 < 0 || row0 + nrows > L) return mf_set_error("mf_layernorm_bwd_inject: rows", -1);
+  const bool v16 = ((uintptr_t)dy % 16 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)dx % 16 == 0) &&
+                   (!dres || ((uintptr_t)dres % 16 == 0 && ldres % 8 == 0)) && lddy % 8 == 0 && ldx % 8 == 0 &&
+                   lddx % 8 == 0 && (uintptr_t)inj_part % 16 == 0;
+  if (!v16 || ln_variant() != 2) return mf_set_error("mf_layernorm_bwd_inject: needs 16-byte aligned rows", -1);
+  const int nblk = mf_layernorm_bwd_blocks(rows);
+  float* dg_part = workspace;
+  float* db_part = workspace + (int64_t)nblk * D;
+  hipStream_t st = (hipStream_t)stream;
+  if (D == 768)
+    ln_bwd2_kernel<768><<<nblk, 256, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, nullptr, gamma, mean, rstd,
+                                              (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows, inj_part,
+                                              L, row0, nrows);
+  else
+    ln_bwd2_kernel<512><<<nblk, 256, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, nullptr, gamma, mean, rstd,
+                                              (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows, inj_part,
+                                              L, row0, nrows);
   MF_CHECK_LAUNCH();
   return 0;
 }

@@ -267,11 +267,13 @@ class _Tower:
             ops.gemm_nt(self.dQKV, self.wt(i, "attn.in_proj_weight"), self.dH, epilogue=ops.EPI_NONE)
             if trainable_w:
                 self._dw(self.dQKV, self.H1, self.g(i, "attn.in_proj_weight"), self.g(i, "attn.in_proj_bias"))
-            self.lnb.bwd(self.dH, self.X[i], self.p(i, "ln_1.weight"), self.mean1[i], self.rstd1[i], dX,
-                           self.g(i, "ln_1.weight"), self.g(i, "ln_1.bias"), dres=dX)
-            if 1 <= i <= n_prompted:
-                ops.prompt_inject_bwd(dX, N, L, self.row0, N_CTX, D, prompt_grads[i - 1], accumulate=False,
-                                      zero_rows=True)
+            if 1 <= i <= n_prompted:  # ln_1 backward + the deep prompt's gradient (its rows of dX) in one pass
+                self.lnb.bwd_inject(self.dH, self.X[i], self.p(i, "ln_1.weight"), self.mean1[i], self.rstd1[i], dX,
+                                    self.g(i, "ln_1.weight"), self.g(i, "ln_1.bias"), dX, prompt_grads[i - 1], L,
+                                    self.row0, N_CTX)
+            else:
+                self.lnb.bwd(self.dH, self.X[i], self.p(i, "ln_1.weight"), self.mean1[i], self.rstd1[i], dX,
+                             self.g(i, "ln_1.weight"), self.g(i, "ln_1.bias"), dres=dX)
 
 
 class MapleEngine:

@@ -208,6 +208,34 @@ class LNGradBatch:
              0, _s())
         return dx
 
+    def bwd_inject(self, dy, x, gamma, mean, rstd, dx, dgamma, dbeta, dres, prompt_grad, L, row0, nrows):
+        """bwd() with the deep-prompt injection backward of the same rows fused in
+        (mf_layernorm_bwd_inject): prompt_grad (fp32 [nrows, D]) = sum over sequences of those rows' dx,
+        reduced in finish() with the LayerNorm partials; the rows of dx are zeroed."""
+        rows, D = dy.shape
+        assert prompt_grad.dtype == torch.float32 and prompt_grad.is_contiguous() and prompt_grad.numel() == nrows * D
+        key = dgamma.data_ptr()
+        if key not in self.ws:
+            nblk = call("mf_layernorm_bwd_blocks", rows)
+            w = torch.empty(2 * nblk * D, device=self.device, dtype=torch.float32)
+            self.ws[key] = w
+            self.descs.append((w.data_ptr(), dgamma.data_ptr(), nblk, D))
+            self.descs.append((w.data_ptr() + 4 * nblk * D, dbeta.data_ptr(), nblk, D))
+            self.max_cols = max(self.max_cols, D)
+            self.dev_descs = None
+        ikey = ("inj", prompt_grad.data_ptr())
+        if ikey not in self.ws:
+            n = rows // L
+            part = torch.empty(n * nrows * D, device=self.device, dtype=torch.float32)
+            self.ws[ikey] = part
+            self.descs.append((part.data_ptr(), prompt_grad.data_ptr(), n, nrows * D))
+            self.max_cols = max(self.max_cols, nrows * D)
+            self.dev_descs = None
+        call("mf_layernorm_bwd_inject", _p(dy), _ld(dy), _p(x), _ld(x), _p(gamma), _p(mean), _p(rstd), _p(dres),
+             _ld(dres) if dres is not None else 0, _p(dx), _ld(dx), _p(self.ws[key]), rows, D, _p(self.ws[ikey]), L,
+             row0, nrows, _s())
+        return dx
+
     def finish(self):
         if not self.descs:
             return

@@ -76,6 +76,15 @@ int mf_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, c
                      void* dx, int64_t lddx, float* dgamma, float* dbeta, float* workspace, int rows, int D,
                      int accumulate, void* stream);
 
+/* Partials-only LayerNorm backward with the deep-prompt injection backward fused in: rows row0..row0+
+ * nrows-1 of each L-row sequence store their dx as fp32 partials inj_part[rows/L][nrows][D] (the prompt
+ * gradient = their sum over sequences, via mf_col_reduce_batch) and a zero dx row.  Replaces
+ * mf_layernorm_bwd + mf_prompt_inject_bwd(zero_rows) on the same rows (clip/model.py:153-159,320-349). */
+int mf_layernorm_bwd_inject(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* gamma,
+                            const float* mean, const float* rstd, const void* dres, int64_t ldres, void* dx,
+                            int64_t lddx, float* workspace, int rows, int D, float* inj_part, int L, int row0,
+                            int nrows, void* stream);
+
 /* dgamma == dbeta == NULL: write the per-block partials only; their reduction is deferred to one
  * mf_col_reduce_batch over all LayerNorms of a backward pass.  desc = {const float* part; float* out;
  * int nblk, C, accumulate, pad} (mf_col_reduce_desc_bytes() bytes each, device memory):
