@@ -54,11 +54,15 @@ SIGNATURES = {
     "mf_fedavg_pack": [P, L, P, L, P, P, P],
     "mf_fedavg_unpack": [P, P, L, P, L, P, P, P],
     "mf_nonfinite_flag": [P, L, I, P, P],
+    "mf_augment_ws_bytes": [I, I, I, I],
+    "mf_augment": [P, L, P, P, P, I, I, I, I, F, F, F, F, F, F, P, I, P, L, P],
 }
 # functions that return a value, not a status
 _VALUE_FUNCS = {"mf_abi_version", "mf_layernorm_bwd_blocks", "mf_colsum_blocks", "mf_optim_chunk_bytes",
                 "mf_optim_chunk_elems", "mf_col_reduce_desc_bytes", "mf_small_linear_desc_bytes",
-                "mf_gemm_splitk_ws_floats"}
+                "mf_gemm_splitk_ws_floats", "mf_augment_ws_bytes"}
+# value functions whose return type is not int
+_RESTYPES = {"mf_augment_ws_bytes": ctypes.c_int64}
 
 _LIB = None
 
@@ -82,7 +86,7 @@ def lib():
     for name, args in SIGNATURES.items():
         fn = getattr(h, name)
         fn.argtypes = args
-        fn.restype = ctypes.c_int
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
     _LIB = h
     return h
 

@@ -172,6 +172,23 @@ int mf_fedavg_unpack(const float* bucket, void* p16, int64_t n16, float* p32, in
                      void* stream);
 int mf_nonfinite_flag(const void* x, int64_t n, int is16, int* flag, void* stream);
 
+/* ---- image transforms (data step before the path) ---------------------
+ * Replaces the CPU transform workers the reference builds from configs/trainers/MaPLeFederated/
+ * *.yaml:8-13 (Dassl build_transform -> torchvision RandomResizedCrop / RandomHorizontalFlip /
+ * Resize + CenterCrop / ToTensor / Normalize on Pillow images, bicubic) and the fp16 cast at
+ * trainers/maple.py:336.  Per image b, geom_host[b*11 ..] = {H, W, y0, x0, ch, cw, RH, RW, oy, ox,
+ * flip} (HOST memory): crop [y0, y0+ch) x [x0, x0+cw) of the HxWx3 uint8 image at src + src_off[b],
+ * resample it Pillow-exactly (interp 0 bicubic, 1 bilinear; 22-bit fixed-point taps, uint8
+ * intermediate) to RH x RW, keep the out_h x out_w window at (oy, ox), flip it horizontally when
+ * flip != 0, and store (u/255 - mean_c)/std_c as fp16 (out_f16) or fp32, planar [B][3][out_h][out_w].
+ * src_off_host / src_off: the same byte offsets on the host (validated) and on the device.
+ * ws: device workspace of mf_augment_ws_bytes(B, out_h, out_w, max crop height) bytes.         */
+int64_t mf_augment_ws_bytes(int B, int out_h, int out_w, int max_rows);
+int mf_augment(const void* src, int64_t src_bytes, const int64_t* src_off_host, const int64_t* src_off,
+               const int* geom_host, int B, int out_h, int out_w, int interp, float mean0, float mean1, float mean2,
+               float std0, float std1, float std2, void* out, int out_f16, void* ws, int64_t ws_bytes,
+               void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -151,7 +151,7 @@ def test_abi_header_matches_binding():
     from federated_multi_modal_amd import _lib
     hdr = (ROOT / "include" / "mapfed.h").read_text()
     hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
-    decls = re.findall(r"\b(?:int|const char\*)\s+(mf_\w+)\s*\(([^)]*)\)\s*;", hdr)
+    decls = re.findall(r"\b(?:int|int64_t|const char\*)\s+(mf_\w+)\s*\(([^)]*)\)\s*;", hdr)
     assert len(decls) >= 25
     for name, args in decls:
         assert name in _lib.exported_symbols(), name

@@ -1,0 +1,172 @@
+"""Image transforms: the device `mf_augment` path against the oracle's
+restatement of Pillow's resampling + torchvision's transforms, and the oracle against Pillow itself.
+
+Bar: bit-exact (uint8 resampling is integer arithmetic; ToTensor/Normalize are correctly rounded
+fp32 ops; the fp16 output is the RNE cast of the fp32 value).  Pillow is importable here and on the
+GPU box (third-party, 12.2); torchvision is not, so its crop sampler is pinned only against the
+oracle's restatement ("parity unpinned" against torchvision itself).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+from oracle import transforms_oracle as T
+
+MEAN = (0.48145466, 0.4578275, 0.40821073)
+STD = (0.26862954, 0.26130258, 0.27577711)
+PIL_INTERP = {"bicubic": Image.BICUBIC, "bilinear": Image.BILINEAR}
+
+
+def _images(seed, shapes):
+    rng = np.random.default_rng(seed)
+    out = []
+    for H, W in shapes:
+        # smooth gradients + noise: exercises both the clipping and the interior of the taps
+        yy, xx = np.mgrid[0:H, 0:W]
+        base = (np.stack([xx * 255.0 / max(W - 1, 1), yy * 255.0 / max(H - 1, 1), (xx + yy) % 256], -1))
+        noise = rng.integers(-60, 61, (H, W, 3))
+        out.append(np.clip(base + noise, 0, 255).astype(np.uint8))
+    return out
+
+
+SHAPES = [(256, 256), (64, 64), (375, 500), (500, 333), (224, 224), (37, 51), (900, 1200), (1, 224)]
+
+
+# ---- oracle pinned against Pillow -------------------------------------------------------------------
+
+@pytest.mark.parametrize("interp", ["bicubic", "bilinear"])
+def test_oracle_resize_matches_pillow(interp):
+    rng = np.random.default_rng(1)
+    cases = [(256, 256, 224, 224), (64, 64, 224, 224), (375, 500, 224, 298), (900, 1200, 224, 224),
+             (10, 7, 3, 19), (224, 224, 224, 224), (1, 5, 4, 4), (300, 40, 224, 29)]
+    cases += [tuple(int(v) for v in rng.integers(1, 320, 4)) for _ in range(12)]
+    for H, W, oh, ow in cases:
+        img = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        ref = np.asarray(Image.fromarray(img).resize((ow, oh), PIL_INTERP[interp]))
+        np.testing.assert_array_equal(T.resize(img, oh, ow, interp), ref, err_msg=f"{(H, W, oh, ow)}")
+
+
+def test_oracle_train_and_test_transform_match_pillow_pipeline():
+    gen = torch.Generator().manual_seed(3)
+    for img in _images(2, SHAPES[:6]):
+        H, W, _ = img.shape
+        i, j, h, w = T.rrc_get_params(H, W, gen)
+        for flip in (False, True):
+            p = Image.fromarray(img).crop((j, i, j + w, i + h)).resize((224, 224), Image.BICUBIC)
+            if flip:
+                p = p.transpose(Image.FLIP_LEFT_RIGHT)
+            ref = T.to_tensor_normalize(np.asarray(p), MEAN, STD)
+            np.testing.assert_array_equal(T.train_transform(img, i, j, h, w, flip, MEAN, STD), ref)
+        rh, rw = T.resize_short_side(H, W, 224)
+        p = Image.fromarray(img).resize((rw, rh), Image.BICUBIC)
+        oy, ox = T.center_crop_offsets(rh, rw, 224, 224)
+        ref = T.to_tensor_normalize(np.asarray(p)[oy:oy + 224, ox:ox + 224], MEAN, STD)
+        np.testing.assert_array_equal(T.test_transform(img, MEAN, STD), ref)
+
+
+# ---- host logic (no GPU) --------------------------------------------------------------------------------
+
+def test_host_crop_sampler_and_sizes_follow_torchvision_restatement():
+    from federated_multi_modal_amd import transforms as D
+    for seed in range(5):
+        g1, g2 = torch.Generator().manual_seed(seed), torch.Generator().manual_seed(seed)
+        for H, W in SHAPES:
+            assert D.rrc_get_params(H, W, g1) == T.rrc_get_params(H, W, g2)
+            assert D.resize_short_side(H, W, 224) == T.resize_short_side(H, W, 224)
+    # the ten-attempt fallback: a 1x224 strip can never hold a 3/4..4/3 crop of >= 8 % of its area
+    i, j, h, w = D.rrc_get_params(1, 224, torch.Generator().manual_seed(0))
+    assert (h, w) == (1, 1) and i == 0 and j == 111
+
+
+def test_geometry_rows_and_config_surface():
+    from types import SimpleNamespace
+    from federated_multi_modal_amd import transforms as D
+    cfg = SimpleNamespace(INPUT=SimpleNamespace(SIZE=(224, 224), INTERPOLATION="bicubic", PIXEL_MEAN=list(MEAN),
+                                                PIXEL_STD=list(STD),
+                                                TRANSFORMS=["random_resized_crop", "random_flip", "normalize"]))
+    tr = D.build_transform(cfg, True, torch.Generator().manual_seed(0))
+    te = D.build_transform(cfg, False)
+    g = tr.geometry(SHAPES)
+    assert g.shape == (len(SHAPES), 11) and set(g[:, 10]) <= {0, 1}
+    assert np.all(g[:, 2] + g[:, 4] <= g[:, 0]) and np.all(g[:, 3] + g[:, 5] <= g[:, 1])
+    gt = te.geometry([(375, 500)])
+    assert gt.tolist() == [[375, 500, 0, 0, 375, 500, 224, 298, 0, 37, 0]]
+    with pytest.raises(NotImplementedError):
+        D.build_transform(SimpleNamespace(INPUT=SimpleNamespace(TRANSFORMS=["colorjitter"])), True)
+
+
+def test_abi_validates_geometry_before_any_launch():
+    from federated_multi_modal_amd import _lib
+    h = _lib.lib()
+    geom = np.array([[64, 64, 10, 0, 60, 64, 224, 224, 0, 0, 0]], np.int32)  # crop rows 10..70 > 64
+    off = np.zeros(1, np.int64)
+    fake = ctypes.c_void_p(16)
+    rc = h.mf_augment(fake, 64 * 64 * 3, off.ctypes.data_as(ctypes.c_void_p), fake,
+                      geom.ctypes.data_as(ctypes.c_void_p), 1, 224, 224, 0, 0, 0, 0, 1, 1, 1, fake, 1, fake,
+                      1 << 30, None)
+    assert rc != 0 and b"crop box" in h.mf_last_error()
+    geom = np.array([[4000, 4000, 0, 0, 4000, 4000, 224, 224, 0, 0, 0]], np.int32)  # 17.9x downscale
+    rc = h.mf_augment(fake, 4000 * 4000 * 3, off.ctypes.data_as(ctypes.c_void_p), fake,
+                      geom.ctypes.data_as(ctypes.c_void_p), 1, 224, 224, 0, 0, 0, 0, 1, 1, 1, fake, 1, fake,
+                      1 << 30, None)
+    assert rc != 0 and b"downscale" in h.mf_last_error()
+    assert h.mf_augment_ws_bytes(0, 224, 224, 1) < 0
+
+
+# ---- device path against the oracle (bit-exact) ------------------------------------------------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("interp", ["bicubic", "bilinear"])
+def test_device_train_transform_bit_exact(dev, interp):
+    from federated_multi_modal_amd import transforms as D
+    imgs = _images(5, SHAPES)
+    packed = D.pack_images(imgs, dev)
+    tr = D.DeviceTransform(True, 224, interp, MEAN, STD, out_dtype=torch.float32,
+                           generator=torch.Generator().manual_seed(7))
+    geom = tr.geometry(packed.shapes)
+    geom[1, 10] = 1  # make sure both flip states are covered
+    geom[2, 10] = 0
+    out32 = tr(packed, geom).cpu().numpy()
+    tr16 = D.DeviceTransform(True, 224, interp, MEAN, STD, out_dtype=torch.float16)
+    out16 = tr16(packed, geom).cpu()
+    for b, img in enumerate(imgs):
+        H, W, y0, x0, ch, cw, RH, RW, oy, ox, flip = geom[b].tolist()
+        crop = img[y0:y0 + ch, x0:x0 + cw]
+        r = T.resize(crop, 224, 224, interp)
+        if flip:
+            r = r[:, ::-1]
+        ref = T.to_tensor_normalize(r, MEAN, STD)
+        np.testing.assert_array_equal(out32[b], ref, err_msg=f"image {b} {geom[b].tolist()}")
+        assert torch.equal(out16[b], torch.from_numpy(ref).half()), b
+
+
+@pytest.mark.gpu
+def test_device_test_transform_bit_exact_against_pillow(dev):
+    from federated_multi_modal_amd import transforms as D
+    imgs = _images(6, SHAPES)
+    packed = D.pack_images(imgs, dev)
+    te = D.DeviceTransform(False, 224, "bicubic", MEAN, STD, out_dtype=torch.float32)
+    out = te(packed).cpu().numpy()
+    for b, img in enumerate(imgs):
+        H, W, _ = img.shape
+        rh, rw = T.resize_short_side(H, W, 224)
+        p = np.asarray(Image.fromarray(img).resize((rw, rh), Image.BICUBIC))
+        oy, ox = T.center_crop_offsets(rh, rw, 224, 224)
+        ref = T.to_tensor_normalize(p[oy:oy + 224, ox:ox + 224], MEAN, STD)
+        np.testing.assert_array_equal(out[b], ref, err_msg=f"image {b} {img.shape}")
+
+
+@pytest.mark.gpu
+def test_device_transform_feeds_the_engine_batch(dev):
+    """The fp16 transform output is the engine's image buffer layout ([B,3,224,224] fp16, contiguous)."""
+    from federated_multi_modal_amd import transforms as D
+    imgs = _images(8, [(256, 256)] * 4)
+    packed = D.pack_images(imgs, dev)
+    out = torch.empty(4, 3, 224, 224, device=dev, dtype=torch.float16)
+    r = D.DeviceTransform(True, generator=torch.Generator().manual_seed(1))(packed, out=out)
+    torch.cuda.synchronize()
+    assert r.data_ptr() == out.data_ptr() and torch.isfinite(out.float()).all()
+    assert D.DeviceTransform(True)(D.pack_images([], dev)).shape == (0, 3, 224, 224)
