@@ -250,6 +250,37 @@ def main():
 
     eval_full, eval_cached = eval_rate(False), eval_rate(True)
 
+    # ---------------- the data step in front of the path: the train transform
+    # (RandomResizedCrop + flip + Normalize -> fp16, Pillow-exact bicubic) on B decoded PatternNet-size
+    # 256x256 RGB images resident in HBM; reported beside `value`, never in it
+    from federated_multi_modal_amd import transforms as dtf
+    rng = np.random.default_rng(seed)
+    packed = dtf.pack_images([rng.integers(0, 256, (256, 256, 3), dtype=np.uint8) for _ in range(B)], dev)
+    tfm = dtf.DeviceTransform(True, generator=torch.Generator().manual_seed(seed))
+    tf_out = torch.empty(B, 3, 224, 224, device=dev, dtype=torch.float16)
+    geoms = [tfm.geometry(packed.shapes) for _ in range(20)]
+    tfm(packed, geoms[0], out=tf_out)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for g in geoms:
+        tfm(packed, g, out=tf_out)
+    ev1.record()
+    torch.cuda.synchronize()
+    tf_us = ev0.elapsed_time(ev1) * 1e3 / len(geoms)
+    tf_bytes = float(np.mean([(g[:, 4] * g[:, 5] * 3).sum() for g in geoms])) + B * 3 * 224 * 224 * 2
+    a0 = time.perf_counter()
+    for _ in range(5):
+        tfm(packed, out=tf_out)  # host draws the crop parameters per batch, as the reference's workers do
+    torch.cuda.synchronize()
+    input_transform = {"images_per_s_device": B / (tf_us * 1e-6), "us_per_batch_device": tf_us,
+                       "images_per_s_with_host_sampling": 5 * B / (time.perf_counter() - a0),
+                       "algorithmic_bytes_per_batch": tf_bytes, "gbs": tf_bytes / (tf_us * 1e-6) / 1e9,
+                       "hbm_frac": tf_bytes / (tf_us * 1e-6) / HBM_PEAK,
+                       "workload": f"train transform, {B} decoded 256x256 RGB images -> fp16 [{B},3,224,224]",
+                       "parity": "bit-exact vs Pillow resize + torchvision ToTensor/Normalize "
+                                 "(tests/test_transforms.py)"}
+
     # ---------------- per-launch roofline of the dominant kernel (eager pass, HIP events on the
     # launching stream around every launch of that kernel during 2 full steps)
     # (towers serialised on one stream here so that no other kernel runs inside a probed launch)
@@ -333,6 +364,7 @@ def main():
         "eot_truncated_mode": eot_mode,
         "eval_images_per_s": {"text_reencoded_per_batch": eval_full, "text_cached_per_pass": eval_cached,
                               "per_gpu": True},
+        "input_transform": input_transform,
         "model_tflops": world * step_flop * args.steps / elapsed / 1e12,
         "model_mfma_frac": world * step_flop * args.steps / elapsed / MFMA_PEAK_F16 / world,
         "loss": loss,

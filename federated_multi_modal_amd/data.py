@@ -98,3 +98,78 @@ class SyntheticClientDataManager:
     @property
     def classnames(self) -> List[str]:
         return self._classnames
+
+
+class _DecodedLoader:
+    """Batches of decoded images run through the device transform (transforms.py): the reference's
+    Dassl loader + per-image CPU transform workers (trainers/client_datamanager.py:21-103)."""
+
+    def __init__(self, packed, labels: torch.Tensor, batch: int, shuffle: bool, drop_last: bool,
+                 gen: torch.Generator, tfm):
+        self.p, self.labels, self.batch, self.shuffle, self.drop_last, self.gen, self.tfm = (
+            packed, labels, batch, shuffle, drop_last, gen, tfm)
+
+    def __len__(self):
+        n = self.labels.numel()
+        return n // self.batch if self.drop_last else (n + self.batch - 1) // self.batch
+
+    def __iter__(self) -> Iterator[Dict[str, object]]:
+        from .transforms import PackedImages
+        n = self.labels.numel()
+        order = torch.randperm(n, generator=self.gen) if self.shuffle else torch.arange(n)
+        for i in range(len(self)):
+            idx = order[i * self.batch:(i + 1) * self.batch]
+            sel = idx.tolist()
+            sub = PackedImages(self.p.data, self.p.offsets_host[sel], [self.p.shapes[k] for k in sel])
+            geom = self.tfm.geometry(sub.shapes)
+            img = self.tfm(sub, geom)
+            idx_d = idx.to(self.labels.device)
+            yield {"img": img, "label": self.labels.index_select(0, idx_d), "caption": [""] * len(sel),
+                   "index": idx_d, "geom": geom}
+
+
+class DecodedClientDataManager:
+    """ClientDataManager over decoded 8-bit RGB images of any sizes (HxWx3 uint8), kept resident in HBM
+    in one packed buffer per split.  Train batches run RandomResizedCrop + flip + Normalize and test
+    batches Resize + CenterCrop + Normalize on the device, bit-identical to the reference's Pillow /
+    torchvision workers (tests/test_transforms.py).  `cfg` supplies INPUT.* (transforms.build_transform);
+    batches are fp32 [B,3,224,224] as the reference's loaders yield them."""
+
+    def __init__(self, client_id: int, classnames: List[str], train_images, train_labels, test_images,
+                 test_labels, train_batch: int, test_batch: int, device, cfg=None, seed: int = 0):
+        from types import SimpleNamespace
+
+        from . import transforms as T
+        self.client_id = client_id
+        self._classnames = list(classnames)
+        self.device = torch.device(device)
+        if cfg is None:
+            cfg = SimpleNamespace(INPUT=SimpleNamespace(SIZE=(224, 224), INTERPOLATION="bicubic",
+                                                        PIXEL_MEAN=list(T.CLIP_MEAN), PIXEL_STD=list(T.CLIP_STD),
+                                                        TRANSFORMS=["random_resized_crop", "random_flip",
+                                                                    "normalize"]))
+        g = torch.Generator().manual_seed(seed * 1000 + client_id)
+        self.train_tfm = T.build_transform(cfg, True, generator=g, out_dtype=torch.float32)
+        self.test_tfm = T.build_transform(cfg, False, out_dtype=torch.float32)
+        tr = T.pack_images(list(train_images), self.device)
+        te = T.pack_images(list(test_images), self.device)
+        ytr = torch.as_tensor(np.asarray(train_labels, np.int64), device=self.device)
+        yte = torch.as_tensor(np.asarray(test_labels, np.int64), device=self.device)
+        if ytr.numel() != len(tr) or yte.numel() != len(te):
+            raise ValueError("one label per image")
+        if ytr.numel() and (int(ytr.min()) < 0 or int(ytr.max()) >= len(classnames)):
+            raise ValueError("train labels outside [0, num_classes)")
+        self.train_loader = _DecodedLoader(tr, ytr, train_batch, True, len(tr) >= train_batch, g, self.train_tfm)
+        self.test_loader = _DecodedLoader(te, yte, test_batch, False, False, g, self.test_tfm)
+
+    @property
+    def num_classes(self) -> int:
+        return len(self._classnames)
+
+    @property
+    def lab2cname(self) -> Dict[int, str]:
+        return {i: c for i, c in enumerate(self._classnames)}
+
+    @property
+    def classnames(self) -> List[str]:
+        return self._classnames

@@ -13,7 +13,7 @@ Here the host only draws the random parameters (torchvision's draw order, on a t
 RandomResizedCrop.get_params, then the flip coin) and packs an 11-int geometry row per image; the
 pixels never leave HBM: one `mf_augment` call crops, resamples Pillow-exactly (22-bit fixed-point
 taps, uint8 intermediate -- bit-identical to PIL.Image.resize), flips, normalises and writes the
-fp16 [B,3,224,224] batch the engine reads.  Images are decoded 8-bit RGB (HxWx3 uint8) of any size,
+[B,3,224,224] batch (fp16, or fp32 for the engine's img_in).  Images are decoded 8-bit RGB (HxWx3 uint8) of any size,
 packed back to back in one device byte buffer (`pack_images`).
 """
 from __future__ import annotations
@@ -156,7 +156,8 @@ class DeviceTransform:
         return out
 
 
-def build_transform(cfg, is_train: bool, generator: torch.Generator = None) -> DeviceTransform:
+def build_transform(cfg, is_train: bool, generator: torch.Generator = None,
+                    out_dtype=torch.float16) -> DeviceTransform:
     """Dassl build_transform(cfg, is_train) for the keys the reference's configs set (INPUT.SIZE,
     INPUT.INTERPOLATION, INPUT.PIXEL_MEAN / PIXEL_STD, INPUT.TRANSFORMS)."""
     inp = cfg.INPUT
@@ -171,4 +172,5 @@ def build_transform(cfg, is_train: bool, generator: torch.Generator = None) -> D
     if is_train and "random_resized_crop" not in choices:
         raise NotImplementedError("train transforms without random_resized_crop")
     return DeviceTransform(is_train, size, interp, mean, std, scale=tuple(getattr(inp, "RRCROP_SCALE", (0.08, 1.0))),
-                           flip_p=0.5 if (is_train and "random_flip" in choices) else 0.0, generator=generator)
+                           flip_p=0.5 if (is_train and "random_flip" in choices) else 0.0, out_dtype=out_dtype,
+                           generator=generator)

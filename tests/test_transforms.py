@@ -170,3 +170,31 @@ def test_device_transform_feeds_the_engine_batch(dev):
     torch.cuda.synchronize()
     assert r.data_ptr() == out.data_ptr() and torch.isfinite(out.float()).all()
     assert D.DeviceTransform(True)(D.pack_images([], dev)).shape == (0, 3, 224, 224)
+
+
+@pytest.mark.gpu
+def test_decoded_client_data_manager_batches_match_oracle(dev):
+    """The loader over decoded images: train batches equal the oracle's transform at the geometry the
+    loader drew; test batches equal Resize + CenterCrop + Normalize; labels follow the sampled indices."""
+    from federated_multi_modal_amd.data import DecodedClientDataManager
+    shapes = [(256, 256), (300, 200), (64, 64), (480, 640), (224, 224), (250, 260)]
+    imgs = _images(9, shapes)
+    labels = [0, 1, 2, 0, 1, 2]
+    dm = DecodedClientDataManager(0, ["a", "b", "c"], imgs, labels, imgs[:3], labels[:3], train_batch=4,
+                                  test_batch=2, device=dev)
+    assert len(dm.train_loader) == 1 and len(dm.test_loader) == 2
+    for batch in dm.train_loader:
+        img = batch["img"].cpu().numpy()
+        assert img.dtype == np.float32 and img.shape == (4, 3, 224, 224)
+        for r, k in enumerate(batch["index"].tolist()):
+            H, W, y0, x0, ch, cw, RH, RW, oy, ox, flip = batch["geom"][r].tolist()
+            ref = T.train_transform(imgs[k], y0, x0, ch, cw, bool(flip), MEAN, STD)
+            np.testing.assert_array_equal(img[r], ref)
+            assert int(batch["label"][r]) == labels[k]
+    seen = 0
+    for batch in dm.test_loader:
+        img = batch["img"].cpu().numpy()
+        for r, k in enumerate(batch["index"].tolist()):
+            np.testing.assert_array_equal(img[r], T.test_transform(imgs[k], MEAN, STD))
+            seen += 1
+    assert seen == 3
