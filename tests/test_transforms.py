@@ -119,9 +119,13 @@ def test_abi_validates_geometry_before_any_launch():
 # ---- device path against the oracle (bit-exact) ------------------------------------------------------
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", ["fused", "3pass"])
 @pytest.mark.parametrize("interp", ["bicubic", "bilinear"])
-def test_device_train_transform_bit_exact(dev, interp):
+def test_device_train_transform_bit_exact(dev, interp, path, monkeypatch):
+    """Both device paths: the fused one-launch kernel (default) and the three-launch path."""
     from federated_multi_modal_amd import transforms as D
+    if path == "3pass":
+        monkeypatch.setenv("MAPFED_AUG_3PASS", "1")
     imgs = _images(5, SHAPES)
     packed = D.pack_images(imgs, dev)
     tr = D.DeviceTransform(True, 224, interp, MEAN, STD, out_dtype=torch.float32,
@@ -198,3 +202,19 @@ def test_decoded_client_data_manager_batches_match_oracle(dev):
             np.testing.assert_array_equal(img[r], T.test_transform(imgs[k], MEAN, STD))
             seen += 1
     assert seen == 3
+
+
+@pytest.mark.gpu
+def test_device_transform_extreme_downscale_falls_back_bit_exact(dev):
+    """A 3400x3400 image resized whole to 224 (63 taps per output index): too many taps for the fused
+    kernel's LDS, so the three-launch path runs; mixed in one batch with an ordinary image."""
+    from federated_multi_modal_amd import transforms as D
+    imgs = _images(11, [(3400, 3400), (256, 256)])
+    packed = D.pack_images(imgs, dev)
+    geom = np.array([[3400, 3400, 0, 0, 3400, 3400, 224, 224, 0, 0, 1],
+                     [256, 256, 16, 8, 200, 240, 224, 224, 0, 0, 0]], np.int32)
+    out = D.DeviceTransform(True, out_dtype=torch.float32)(packed, geom).cpu().numpy()
+    for b, img in enumerate(imgs):
+        H, W, y0, x0, ch, cw, RH, RW, oy, ox, flip = geom[b].tolist()
+        ref = T.train_transform(img, y0, x0, ch, cw, bool(flip), MEAN, STD)
+        np.testing.assert_array_equal(out[b], ref, err_msg=f"image {b}")
