@@ -218,3 +218,24 @@ def test_device_transform_extreme_downscale_falls_back_bit_exact(dev):
         H, W, y0, x0, ch, cw, RH, RW, oy, ox, flip = geom[b].tolist()
         ref = T.train_transform(img, y0, x0, ch, cw, bool(flip), MEAN, STD)
         np.testing.assert_array_equal(out[b], ref, err_msg=f"image {b}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stage", [True, False])
+def test_device_train_transform_small_images_staged_bit_exact(dev, stage, monkeypatch):
+    """PatternNet / EuroSAT-size images: the fused kernel reads the crop rows from global memory
+    (default), or with MAPFED_AUG_STAGE stages each band's crop rows in LDS first.  Both bit-exact."""
+    from federated_multi_modal_amd import transforms as D
+    if stage:
+        monkeypatch.setenv("MAPFED_AUG_STAGE", "1")
+    shapes = [(256, 256), (64, 64), (224, 224), (37, 51), (250, 200), (256, 256)]
+    imgs = _images(12, shapes)
+    packed = D.pack_images(imgs, dev)
+    tr = D.DeviceTransform(True, out_dtype=torch.float32, generator=torch.Generator().manual_seed(4))
+    geom = tr.geometry(packed.shapes)
+    geom[0, 10], geom[1, 10] = 1, 0
+    out = tr(packed, geom).cpu().numpy()
+    for b, img in enumerate(imgs):
+        H, W, y0, x0, ch, cw, RH, RW, oy, ox, flip = geom[b].tolist()
+        ref = T.train_transform(img, y0, x0, ch, cw, bool(flip), MEAN, STD)
+        np.testing.assert_array_equal(out[b], ref, err_msg=f"image {b} {geom[b].tolist()}")
