@@ -53,6 +53,7 @@ SIGNATURES = {
     "mf_sgd_step": [P, P, P, L, I, P, P, P],
     "mf_fedavg_pack": [P, L, P, L, P, P, P],
     "mf_fedavg_unpack": [P, P, L, P, L, P, P, P],
+    "mf_fedavg_reduce_ordered": [P, I, L, L, P, P],
     "mf_nonfinite_flag": [P, L, I, P, P],
     "mf_augment_ws_bytes": [I, I, I, I],
     "mf_augment": [P, L, P, P, P, I, I, I, I, F, F, F, F, F, F, P, I, P, L, P],

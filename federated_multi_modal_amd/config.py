@@ -162,7 +162,9 @@ def get_cfg_default() -> CfgNode:
                                                      N_DOMAIN=0, N_INS=16)),
                                 TEST=CfgNode(dict(SAMPLER="SequentialSampler", BATCH_SIZE=32))))
     C.MODEL = CfgNode(dict(INIT_WEIGHTS="", NUM_CLASSES=0,
-                           BACKBONE=CfgNode(dict(NAME="", PRETRAINED=True)),
+                           # PATH (MI355X addition): the local CLIP checkpoint clip._download would fetch for
+                           # NAME (trainers/maple.py:21-40); empty -> clip's download cache, else synthetic
+                           BACKBONE=CfgNode(dict(NAME="", PRETRAINED=True, PATH="")),
                            HEAD=CfgNode(dict(NAME="", HIDDEN_LAYERS=(), ACTIVATION="relu", BN=True, DROPOUT=0.0))))
     C.OPTIM = CfgNode(dict(NAME="adam", LR=0.0003, WEIGHT_DECAY=5e-4, MOMENTUM=0.9, SGD_DAMPNING=0,
                            SGD_NESTEROV=False, RMSPROP_ALPHA=0.99, ADAM_BETA1=0.9, ADAM_BETA2=0.999,
@@ -185,7 +187,10 @@ def extend_cfg(cfg: CfgNode) -> None:
     cfg.TRAINER.IVLP = CfgNode(dict(N_CTX_VISION=2, N_CTX_TEXT=2, CTX_INIT="a photo of a", PREC="fp16",
                                     PROMPT_DEPTH_VISION=9, PROMPT_DEPTH_TEXT=9))
     cfg.TRAINER.VPT = CfgNode(dict(N_CTX_VISION=2, CTX_INIT="a photo of a", PREC="fp16", PROMPT_DEPTH_VISION=1))
-    cfg.FED = CfgNode(dict(NUM_CLIENTS=2, NUM_ROUNDS=30, LOCAL_EPOCHS=10))
+    cfg.FED = CfgNode(dict(NUM_CLIENTS=2, NUM_ROUNDS=30, LOCAL_EPOCHS=10,
+                           # MI355X additions (federated.py): the bucket exchange -- "ordered" (all_gather +
+                           # client-order sum, bit-identical to safe_average_weights) or "allreduce"
+                           AGGREGATION="ordered"))
 
 
 def reset_cfg(cfg: CfgNode, args) -> None:

@@ -60,7 +60,11 @@ __global__ void loss_kernel(const f16* __restrict__ logits, const f16* __restric
   const float sc = fminf(expf(logit_scale[0]), 100.f);
   for (int b = w; b < B; b += nw) {
     const f16* lr = logits + (int64_t)b * K;
-    const int y = (int)label[b];
+    // a label outside [0, K) (the reference asserts, trainers/maple.py:352-353) is not indexed: the row's
+    // loss becomes NaN, so the step is flagged non-finite and its update skipped
+    const int y_raw = (int)label[b];
+    const bool y_bad = y_raw < 0 || y_raw >= K;
+    const int y = y_bad ? 0 : y_raw;
     float mx = -INFINITY;
     for (int k = lane; k < K; k += 64) mx = fmaxf(mx, (float)lr[k]);
     mx = wave_max(mx);
@@ -92,7 +96,7 @@ __global__ void loss_kernel(const f16* __restrict__ logits, const f16* __restric
     }
     c = r16(wave_sum(c));
     if (lane == 0) {
-      s_ce[b] = -logp_y;
+      s_ce[b] = y_bad ? __builtin_nanf("") : -logp_y;
       s_cos[b] = c;
       cos_out[2 * b] = nu;
       cos_out[2 * b + 1] = nv;
@@ -122,7 +126,8 @@ __global__ void dimg_kernel(const f16* __restrict__ dmm, const f16* __restrict__
                             const int64_t* __restrict__ label, const f16* __restrict__ soft_rows,
                             const float* __restrict__ cos_norms, int B, int K, int D, f16* __restrict__ dimg_n) {
   const int b = blockIdx.x;
-  const f16* trow = soft_rows ? soft_rows + (int64_t)b * D : txt_n + (int64_t)label[b] * D;
+  const int y_raw = soft_rows ? 0 : (int)label[b];
+  const f16* trow = soft_rows ? soft_rows + (int64_t)b * D : txt_n + (int64_t)((y_raw < 0 || y_raw >= K) ? 0 : y_raw) * D;
   const float dcos = r16(-0.5f / (float)B);
   const float nu = cos_norms[2 * b], nv = cos_norms[2 * b + 1];
   __shared__ float red[4];

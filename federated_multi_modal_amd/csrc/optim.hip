@@ -117,13 +117,15 @@ __global__ __launch_bounds__(1024) void clip_coef_kernel(const float* __restrict
   }
 }
 
-// hyper = {lr, momentum, weight_decay, first_step (1.0 = momentum buffer not yet created)}: read from
-// device memory so a captured step replays with the current schedule value.
+// hyper = {lr, momentum, weight_decay, first_step (1.0 = momentum buffer not yet created), halt}: read from
+// device memory so a captured step replays with the current schedule value.  halt != 0 (a non-finite loss
+// earlier in the epoch or in this step) leaves parameters, gradients and momentum untouched: the reference
+// raises at the first non-finite loss before its backward (trainers/maple.py:375-376), so no update follows.
 template <typename T>
 __global__ void sgd_kernel(T* __restrict__ p, T* __restrict__ g, T* __restrict__ buf, int64_t n,
                            const float* __restrict__ coef_ptr, const float* __restrict__ hyper) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || hyper[4] != 0.f) return;
   const float coef = coef_ptr[1];
   const float lr = hyper[0], momentum = hyper[1], wd = hyper[2];
   const bool first = hyper[3] != 0.f;
@@ -147,7 +149,7 @@ __global__ void sgd8_kernel(T* __restrict__ p, T* __restrict__ g, T* __restrict_
                             const float* __restrict__ coef_ptr, const float* __restrict__ hyper) {
   using V = typename std::conditional<std::is_same<T, f16>::value, f16x8, float __attribute__((ext_vector_type(8)))>::type;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n8) return;
+  if (i >= n8 || hyper[4] != 0.f) return;
   const float coef = coef_ptr[1];
   const float lr = hyper[0], momentum = hyper[1], wd = hyper[2];
   const bool first = hyper[3] != 0.f;
@@ -212,6 +214,32 @@ __global__ void unpack_kernel(const float* __restrict__ bucket, f16* __restrict_
   }
 }
 
+// out[i] = (((g_0[i] + g_1[i]) + g_2[i]) + ...) in client order, g_c = gathered + c * stride: the
+// per-key torch.stack(...) sum of trainers/maple_fed.py:311-314 in the order the reference stacks its
+// clients, whatever order the collective delivered them in (8 floats per thread, fp32 accumulation)
+__global__ void reduce_ordered_kernel(const float* __restrict__ g, int nclients, int64_t stride, int64_t n,
+                                      float* __restrict__ out) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= n) return;
+  if (i + 4 <= n && stride % 4 == 0 && ((uintptr_t)g % 16) == 0 && ((uintptr_t)out % 16) == 0) {
+    float4 acc = *(const float4*)(g + i);
+    for (int c = 1; c < nclients; ++c) {
+      const float4 v = *(const float4*)(g + (int64_t)c * stride + i);
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    *(float4*)(out + i) = acc;
+  } else {
+    for (int64_t j = i; j < n && j < i + 4; ++j) {
+      float acc = g[j];
+      for (int c = 1; c < nclients; ++c) acc += g[(int64_t)c * stride + j];
+      out[j] = acc;
+    }
+  }
+}
+
 // flag[0] |= 1 if any element is NaN/Inf
 __global__ void nonfinite_kernel(const void* __restrict__ x, int64_t n, int is16, int* __restrict__ flag) {
   int bad = 0;
@@ -272,6 +300,15 @@ extern "C" int mf_fedavg_unpack(const float* bucket, void* p16, int64_t n16, flo
                                 float* g32, void* stream) {
   if (n16 + n32 <= 0) return 0;
   unpack_kernel<<<nblk(n16 + n32), 256, 0, (hipStream_t)stream>>>(bucket, (f16*)p16, n16, p32, n32, (f16*)g16, g32);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_fedavg_reduce_ordered(const float* gathered, int nclients, int64_t stride, int64_t n, float* out,
+                                        void* stream) {
+  if (nclients < 1 || n < 0 || stride < n) return mf_set_error("mf_fedavg_reduce_ordered: bad sizes", -1);
+  if (n == 0) return 0;
+  reduce_ordered_kernel<<<nblk((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(gathered, nclients, stride, n, out);
   MF_CHECK_LAUNCH();
   return 0;
 }

@@ -149,6 +149,12 @@ def engine_state_from_clip(clip_sd: Dict[str, np.ndarray], cfg: EngineConfig,
     for k, v in pl.items():
         out["prompt_learner." + k] = np.asarray(v, dtype=np.float32)
     out["logit_scale"] = np.array(math.log(1 / 0.07), dtype=np.float32)
+    # CLIP's own tensors the towers do not read but CustomCLIP.state_dict() carries as clip_model2.*
+    # aliases (trainers/maple.py:229): its logit_scale and the token-embedding table
+    if "logit_scale" in clip_sd:
+        out["clip_model2.logit_scale"] = np.asarray(clip_sd["logit_scale"], dtype=np.float32)
+    if "token_embedding.weight" in clip_sd:
+        out["clip_model2.token_embedding.weight"] = np.asarray(clip_sd["token_embedding.weight"], dtype=np.float32)
     return out
 
 
@@ -294,14 +300,23 @@ class MapleEngine:
         if shared is None:
             vals = state if state is not None else synthetic_state(cfg)
             self._build_params(vals)
+            # clip_model2.logit_scale (CLIP's, not MaPLe's) and clip_model2.token_embedding.weight: host
+            # copies for the reference's state-dict key set; the table is generated on first use when the
+            # weights are the seeded synthetic CLIP
+            self.clip_logit_scale = torch.tensor(float(vals.get("clip_model2.logit_scale", math.log(1 / 0.07))),
+                                                 dtype=F32)
+            tok = vals.get("clip_model2.token_embedding.weight")
+            self._token_table = None if tok is None else torch.as_tensor(np.asarray(tok, dtype=np.float32))
             self._build_text_constants()
-            self.hyper = torch.tensor([0.0, cfg.momentum, cfg.weight_decay, 1.0], device=self.device, dtype=F32)
+            # {lr, momentum, weight_decay, first_step, halt}: read by the SGD kernels from device memory
+            self.hyper = torch.tensor([0.0, cfg.momentum, cfg.weight_decay, 1.0, 0.0], device=self.device, dtype=F32)
         else:
             assert shared.K == self.K and shared.J == self.J and shared.device == self.device
             assert shared.cfg.eot_truncate == cfg.eot_truncate
             for a in ("n16", "n32", "flat16", "flat32", "gflat16", "gflat32", "mom16", "mom32", "P", "G",
                       "trainable_names", "conv_w", "chunks", "nchunks", "norm_part", "clip_out", "WT", "tokenized",
-                      "token_prefix", "token_suffix", "token_suffix_run", "text_len", "eot_rows", "hyper"):
+                      "token_prefix", "token_suffix", "token_suffix_run", "text_len", "eot_rows", "hyper",
+                      "clip_logit_scale", "_token_table"):
                 setattr(self, a, getattr(shared, a))
         G2 = d.grid * d.grid
         self.Lv = G2 + 1 + cfg.n_ctx
@@ -657,12 +672,22 @@ class MapleEngine:
         self.hyper[3] = 1.0
 
     def optimizer_step(self):
-        """clip_grad_norm_(1.0) + SGD.step (trainers/maple.py:592-598), all on device."""
+        """clip_grad_norm_(1.0) + SGD.step (trainers/maple.py:592-598), all on device.
+
+        A non-finite loss latches hyper[4] (halt): the reference raises RuntimeError("NaN/Inf in total
+        loss") at that step before its backward (trainers/maple.py:375-376), so neither that step nor any
+        later one of the epoch updates the weights; the SGD kernels skip while halt is set.  The trainer
+        clears it at the start of an epoch and reports the failure (MaPLe.run_epoch)."""
+        torch.maximum(self.hyper[4:5], self.loss_out[3:4], out=self.hyper[4:5])
         ops.clip_grad_norm(self.gflat16, self.gflat32, self.chunks, self.nchunks, self.cfg.max_grad_norm,
                            self.norm_part, self.clip_out)
         ops.sgd_step(self.flat16, self.gflat16, self.mom16, self.clip_out, self.hyper)
         ops.sgd_step(self.flat32, self.gflat32, self.mom32, self.clip_out, self.hyper)
-        self.hyper[3:4].zero_()  # a device fill, legal inside graph capture
+        # the momentum buffers now exist (first_step -> 0) unless the update was skipped
+        self.hyper[3:4].mul_(self.hyper[4:5])  # device ops, legal inside graph capture
+
+    def clear_halt(self):
+        self.hyper[4:5].zero_()
 
     def train_step(self):
         self.forward_backward()
@@ -697,33 +722,64 @@ class MapleEngine:
         clip_model2.* aliases and buffers, see reference_state_dict)."""
         return {n: t for n, t in self.P.items()}
 
+    def token_embedding_table(self) -> torch.Tensor:
+        """CLIP's token-embedding table [vocab, 512] fp32 (host): the checkpoint's, or the seeded
+        synthetic one (the same values the prompt rows were taken from)."""
+        if self._token_table is None:
+            d = self.cfg.dims
+            tab = syn.fp16_round(0.02 * syn.normal(self.cfg.seed, "token_embedding.weight", d.vocab_size * d.text_width))
+            self._token_table = torch.from_numpy(tab.reshape(d.vocab_size, d.text_width))
+        return self._token_table
+
+    @staticmethod
+    def alias_of(name: str) -> Optional[str]:
+        """The clip_model2.* alias of a tower parameter (CustomCLIP keeps clip_model as clip_model2 and
+        its visual / text modules as image_encoder / text_encoder, trainers/maple.py:221-229)."""
+        if name.startswith("image_encoder."):
+            return "clip_model2.visual." + name[len("image_encoder."):]
+        if name.startswith("text_encoder."):
+            return "clip_model2." + name[len("text_encoder."):]
+        return None
+
     def reference_state_dict(self) -> Dict[str, torch.Tensor]:
         """The reference's full CustomCLIP state-dict key set (trainers/maple.py:221-229): parameters,
         the prompt learner's token_prefix/suffix buffers and the clip_model2.* aliases of the CLIP
-        weights the towers share (634 keys at J=9, token_embedding excluded)."""
+        modules (616 keys at J=3, 634 at J=9; tests/golden/state_dict_keys.json)."""
         out = dict(self.state_dict())
         out["prompt_learner.token_prefix"] = self.token_prefix
         out["prompt_learner.token_suffix"] = self.token_suffix
         for n, t in self.P.items():
-            if n.startswith("image_encoder."):
-                out["clip_model2.visual." + n[len("image_encoder."):]] = t
-            elif n.startswith("text_encoder."):
-                out["clip_model2." + n[len("text_encoder."):]] = t
-        out["clip_model2.logit_scale"] = self.P["logit_scale"]
+            a = self.alias_of(n)
+            if a is not None:
+                out[a] = t
+        out["clip_model2.logit_scale"] = self.clip_logit_scale
+        out["clip_model2.token_embedding.weight"] = self.token_embedding_table()
         return out
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
-        """load_state_dict of the reference model (trainers/maple_fed.py:329): every parameter name
-        must be present when strict; values are cast to each parameter's dtype."""
-        missing = [n for n in self.P if n not in sd]
-        if strict and missing:
-            raise RuntimeError(f"Missing key(s) in state_dict: {missing[:5]}...")
+        """load_state_dict of the reference model (trainers/maple_fed.py:329): with strict, every key of
+        reference_state_dict() must be present and no other; values are cast to each tensor's dtype.  A
+        tower parameter absent under its own name is taken from its clip_model2.* alias."""
+        own = set(self.reference_state_dict()) if strict else None
+        if strict:
+            missing = sorted(own - set(sd))
+            unexpected = sorted(set(sd) - own)
+            if missing or unexpected:
+                raise RuntimeError(f"Error(s) in loading state_dict: missing keys {missing[:5]} "
+                                   f"({len(missing)}), unexpected keys {unexpected[:5]} ({len(unexpected)})")
         frozen_changed = False
         with torch.no_grad():
             for n, t in self.P.items():
-                if n in sd:
-                    t.copy_(torch.as_tensor(sd[n]).reshape(t.shape).to(device=t.device, dtype=t.dtype))
+                src = sd.get(n)
+                if src is None and self.alias_of(n) is not None:
+                    src = sd.get(self.alias_of(n))
+                if src is not None:
+                    t.copy_(torch.as_tensor(src).reshape(t.shape).to(device=t.device, dtype=t.dtype))
                     frozen_changed |= n not in self.trainable_names
+            if "clip_model2.logit_scale" in sd:
+                self.clip_logit_scale.copy_(torch.as_tensor(sd["clip_model2.logit_scale"]).float().cpu())
+            if "clip_model2.token_embedding.weight" in sd:
+                self._token_table = torch.as_tensor(sd["clip_model2.token_embedding.weight"]).float().cpu().clone()
             if "prompt_learner.token_prefix" in sd:
                 self.token_prefix.copy_(sd["prompt_learner.token_prefix"])
                 self.token_suffix.copy_(sd["prompt_learner.token_suffix"])

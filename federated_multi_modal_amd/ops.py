@@ -440,5 +440,12 @@ def fedavg_unpack(bucket, p16, p32, g16=None, g32=None):
     call("mf_fedavg_unpack", _p(bucket), _p(p16), p16.numel(), _p(p32), p32.numel(), _p(g16), _p(g32), _s())
 
 
+def fedavg_reduce_ordered(gathered, nclients, out):
+    """out = sum over clients (in client order) of gathered.view(nclients, -1)[:, :out.numel()]."""
+    stride = gathered.numel() // nclients
+    assert gathered.numel() == stride * nclients and out.numel() <= stride
+    call("mf_fedavg_reduce_ordered", _p(gathered), nclients, stride, out.numel(), _p(out), _s())
+
+
 def nonfinite_flag(x, flag):
     call("mf_nonfinite_flag", _p(x), x.numel(), int(x.dtype == torch.float16), _p(flag), _s())

@@ -148,6 +148,7 @@ class MaPLe(TrainerX):
             self.device = torch.device(device)
         self.lr_history: List[float] = []
         self.grad_norms: List[float] = []
+        self.batch_idx = 0
         self._built = False
         self.check_cfg(cfg)
         super().__init__(cfg)
@@ -169,16 +170,20 @@ class MaPLe(TrainerX):
 
     def build_model(self):
         """trainers/maple.py:421-524: CLIP ViT-B/16 + CustomCLIP, freeze policy (:447-479), SGD + LR
-        schedule (:498-499).  Weights: MODEL.INIT_WEIGHTS (a CLIP checkpoint / state dict file) when
-        given, else the seeded synthetic CLIP (the download of clip/clip.py:29-68 is offline)."""
+        schedule (:498-499).  Backbone: load_clip_to_cpu (:21-40) reads the checkpoint clip._download
+        caches for MODEL.BACKBONE.NAME; it is taken from MODEL.BACKBONE.PATH or that cache
+        (~/.cache/clip/<file>), else the seeded synthetic CLIP (there is no network).  MODEL.INIT_WEIGHTS
+        is then applied on top as Dassl's load_pretrained_weights does (:489-490): a CustomCLIP / MaPLe
+        checkpoint loaded by key match (see load_pretrained_weights below)."""
         if self._built:
             return
         cfg = self.cfg
         mcfg = cfg.TRAINER.MAPLE
         classnames = self.classnames
         state = None
-        if cfg.MODEL.INIT_WEIGHTS:
-            state = _load_clip_weights(cfg.MODEL.INIT_WEIGHTS, cfg, classnames, mcfg)
+        backbone = _backbone_file(cfg)
+        if backbone:
+            state = _load_clip_weights(backbone, cfg, classnames, mcfg)
         ecfg = EngineConfig(batch=cfg.DATALOADER.TRAIN_X.BATCH_SIZE, classnames=list(classnames),
                             prompt_depth=mcfg.PROMPT_DEPTH, seed=max(cfg.SEED, 0), n_ctx=mcfg.N_CTX,
                             ctx_init=mcfg.CTX_INIT, momentum=cfg.OPTIM.MOMENTUM,
@@ -188,6 +193,8 @@ class MaPLe(TrainerX):
         self.engine = MapleEngine(ecfg, device=self.device, state=state)
         self._eval_engine: Optional[MapleEngine] = None
         self.model = _ModelView(self.engine)
+        if cfg.MODEL.INIT_WEIGHTS:
+            load_pretrained_weights(self.model, cfg.MODEL.INIT_WEIGHTS)
         self.optim = HostLR(cfg.OPTIM)          # param_groups[0]['lr'] and the scheduler
         self.sched = self.optim.sched
         self.scaler = None
@@ -195,6 +202,7 @@ class MaPLe(TrainerX):
         self._graphs = {}
         self._loss_sum = torch.zeros(1, device=self.device)
         self._bad = torch.zeros(1, device=self.device)
+        self._ok = torch.zeros(1, device=self.device)   # steps of the epoch before its first non-finite loss
         self._acc = torch.zeros(2, device=self.device)
         self.lr_history = [self.optim.lr]
         self._built = True
@@ -216,6 +224,11 @@ class MaPLe(TrainerX):
         e = self.engine
         if image.shape[0] != e.B:
             raise ValueError(f"batch of {image.shape[0]} images; the client engine is built for {e.B}")
+        if not label.is_floating_point() and label.device.type == "cpu" and label.numel():
+            # trainers/maple.py:352-353 (label sanity); device labels are range-checked by the loss kernels,
+            # which flag the step as non-finite instead of indexing out of bounds
+            if int(label.min()) < 0 or int(label.max()) >= e.K:
+                raise AssertionError("Label index out of bounds")
         e.img_in.copy_(image, non_blocking=True)
         e.set_labels(label)  # float labels -> KL branch (trainers/maple.py:356-360)
 
@@ -234,35 +247,58 @@ class MaPLe(TrainerX):
             g.replay()
         self._loss_sum.add_(e.loss_out[0:1])
         self._bad.add_(e.loss_out[3:4])
+        self._ok.add_((self._bad == 0).float())
 
     def forward_backward(self, batch):
-        """trainers/maple.py:547-627: returns {"loss": float} (one host sync, like loss.item())."""
+        """trainers/maple.py:547-627: returns {"loss": float} (one host sync, like loss.item()).  A
+        non-finite loss raises RuntimeError("NaN/Inf in total loss") with the weights untouched by that
+        step (the reference raises before its backward, :375-376)."""
         image, label, _ = self.parse_batch_train(batch)
         self.check_tensor_validity(image, "input image")
         self.check_tensor_validity(label, "input label")
-        before = float(self._loss_sum.item())
+        if not label.is_floating_point() and label.numel():  # trainers/maple.py:352-353
+            lo_hi = torch.stack([label.min(), label.max()]).tolist()
+            if lo_hi[0] < 0 or lo_hi[1] >= self.engine.K:
+                raise AssertionError("Label index out of bounds")
+        self.engine.clear_halt()
         self._step_async(batch)
-        loss = float(self._loss_sum.item()) - before
-        if self.engine.loss_out[3].item() != 0.0:
+        out = self.engine.loss_out.tolist()
+        loss = out[0]
+        if out[3] != 0.0:
             raise RuntimeError("NaN/Inf in total loss")
         # the grad-norm log of trainers/maple.py:605-612 (norm of the clipped gradients): total * coef
         total, coef = self.engine.clip_out[:2].tolist()
         self.grad_norms.append(total * coef)
         return {"loss": loss}
 
-    def run_epoch(self, epoch):
-        """trainers/maple.py:629-653: one pass over the train loader, update_lr, test()."""
+    def run_epoch(self, epoch, before_test=None):
+        """trainers/maple.py:629-653: one pass over the train loader, update_lr, test().
+
+        No host synchronisation per step: the losses and the non-finite flag accumulate on the device
+        and are read once after the pass.  A non-finite loss halts the weight updates from that step on
+        (MapleEngine.optimizer_step) and raises RuntimeError("NaN/Inf in total loss") here, as the
+        reference raises at that step (:375-376, re-raised at :627); total_batches / batch_idx then count
+        up to the failing batch.  before_test: called after update_lr, before test() (the federated loop
+        starts the FedAvg exchange there so it overlaps the local test)."""
         self.model.train()
         self._loss_sum.zero_()
         self._bad.zero_()
+        self._ok.zero_()
+        self.engine.clear_halt()
         steps = 0
+        start = self.total_batches
         for batch_idx, batch in enumerate(self.dm.train_loader):
             self.batch_idx = batch_idx
             self._step_async(batch)
             steps += 1
-        if self._bad.item() != 0.0:  # NaN/Inf loss in this epoch (trainers/maple.py:375-376)
+        bad, ok = self._bad.item(), int(self._ok.item())
+        if bad != 0.0:  # NaN/Inf loss in this epoch (trainers/maple.py:375-376)
+            self.total_batches = start + ok + 1
+            self.batch_idx = ok
             raise RuntimeError("NaN/Inf in total loss")
         self.update_lr()
+        if before_test is not None:
+            before_test()
         local = self.test()
         avg_loss = float(self._loss_sum.item()) / max(1, steps)
         print(f"[Client {self.client_id}] Epoch {epoch} done. Loss={avg_loss:.4f}, Acc={local['accuracy']:.2f}%")
@@ -329,11 +365,59 @@ class MaPLe(TrainerX):
             self._models[name].load_state_dict(sd, strict=False)
 
 
+_CLIP_FILES = {"ViT-B/16": "ViT-B-16.pt", "ViT-B/32": "ViT-B-32.pt", "ViT-L/14": "ViT-L-14.pt"}
+
+
+def _backbone_file(cfg) -> str:
+    """The CLIP checkpoint load_clip_to_cpu would read (trainers/maple.py:21-40 -> clip._download, whose
+    cache is ~/.cache/clip/<basename of the URL>, clip/clip.py:39-44): MODEL.BACKBONE.PATH, else that
+    cache file when present, else "" (seeded synthetic CLIP)."""
+    path = cfg.MODEL.BACKBONE.get("PATH", "") if hasattr(cfg.MODEL.BACKBONE, "get") else ""
+    if path:
+        if not osp.isfile(path):
+            raise FileNotFoundError(f"MODEL.BACKBONE.PATH {path} not found")
+        return path
+    name = _CLIP_FILES.get(cfg.MODEL.BACKBONE.NAME)
+    if name:
+        cached = osp.join(osp.expanduser("~/.cache/clip"), name)
+        if osp.isfile(cached):
+            return cached
+    return ""
+
+
+def load_pretrained_weights(model, weight_path):
+    """Dassl's load_pretrained_weights (called at trainers/maple.py:489-490): read a checkpoint (a dict
+    with "state_dict", or a state dict), drop a "module." prefix, keep the keys the model has with the
+    same shape, load them; report what was discarded.  Loaded with weights_only=True (no code runs)."""
+    ckpt = torch.load(weight_path, map_location="cpu", weights_only=True)
+    sd = ckpt["state_dict"] if isinstance(ckpt, dict) and "state_dict" in ckpt else ckpt
+    own = model.state_dict()
+    matched, discarded = {}, []
+    for k, v in sd.items():
+        k = k[7:] if k.startswith("module.") else k
+        if k in own and tuple(own[k].shape) == tuple(v.shape):
+            matched[k] = v
+        else:
+            discarded.append(k)
+    if not matched:
+        print(f"Cannot load {weight_path} (check the key names manually)")
+        return
+    model.load_state_dict(matched, strict=False)
+    print(f"Successfully loaded pretrained weights from {weight_path}")
+    if discarded:
+        print(f"** The following layers are discarded due to unmatched keys or layer size: {discarded[:10]}")
+
+
 def _load_clip_weights(path, cfg, classnames, mcfg):
-    """A CLIP state dict saved with torch.save (loaded with weights_only=True: no code runs)."""
+    """A CLIP checkpoint: a state dict saved with torch.save (loaded with weights_only=True: no code
+    runs), or the TorchScript archive clip._download fetches (its parameters are read through
+    torch.jit.load, as load_clip_to_cpu does first, trainers/maple.py:27-31)."""
     import numpy as np
     from .engine import engine_state_from_clip
-    sd = torch.load(path, map_location="cpu", weights_only=True)
+    try:
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+    except Exception:  # the official archives are TorchScript (zip with code/), not a plain state dict
+        sd = torch.jit.load(path, map_location="cpu").state_dict()
     if isinstance(sd, dict) and "state_dict" in sd:
         sd = sd["state_dict"]
     ecfg = EngineConfig(batch=1, classnames=list(classnames), prompt_depth=mcfg.PROMPT_DEPTH, seed=max(cfg.SEED, 0),
@@ -401,12 +485,19 @@ class MaPLeFederated(TrainerX):
                                       dm=self.client_data_managers[i], device=self.device))
         c0 = self.clients[0]
         self.register_model("MultiModalPromptLearner_Aggregator", c0.model, None, None)
-        self.fed = [FedAvgBucket(c.engine) for c in self.clients]
+        mode = self.cfg.FED.get("AGGREGATION", "ordered") if hasattr(self.cfg.FED, "get") else "ordered"
+        self.fed = [FedAvgBucket(c.engine, mode=mode) for c in self.clients]
         self.global_weights = self.clients[0].model.state_dict()
 
     # ---------------------------------------------------------------- round loop
     def train(self):
-        """trainers/maple_fed.py:228-303."""
+        """trainers/maple_fed.py:228-303.
+
+        FedAvg overlap: a client's bucket is packed and its exchange (RCCL all_gather or all_reduce,
+        federated.py) launched right after its last local epoch's SGD steps and LR update, before that
+        epoch's test() (trainers/maple.py:646), which only reads the weights; the collective flies while
+        the test batches run and is waited for after the client loop.  The result equals the reference's
+        FedAvg-after-training order: the test reads the same local weights and the bucket holds them."""
         for round_idx in range(self.num_rounds):
             print(f"\n--- Federated Round {round_idx + 1}/{self.num_rounds} ---")
             self.broadcast_weights()
@@ -416,18 +507,25 @@ class MaPLeFederated(TrainerX):
                 trainer.epoch = round_idx * self.local_epochs
                 trainer.max_epoch = (round_idx + 1) * self.local_epochs
                 last = 0.0
+                started = []
+
+                def start_fedavg(fed=fed, started=started):
+                    fed.start(collective=self.distributed)
+                    started.append(True)
                 try:
                     for ep in range(trainer.epoch, trainer.max_epoch):
-                        last = trainer.run_epoch(ep).get("avg_loss", 0.0)
+                        hook = start_fedavg if ep == trainer.max_epoch - 1 else None
+                        last = trainer.run_epoch(ep, before_test=hook).get("avg_loss", 0.0)
                     round_losses.append(last)
                 except RuntimeError as err:
                     print(f"Client {trainer.client_id} failed training: {err}")
                     self.nan_stats["failed_clients"].append(trainer.client_id)
                     failed_local.append(trainer.client_id)
-                    fed.flag.fill_(1)   # excluded from the average
+                if not started:  # failed, or no local epochs: pack (excluded when failed) and exchange now
+                    fed.start(collective=self.distributed, failed=trainer.client_id in failed_local)
             if round_losses:
                 print(f"[Round {round_idx + 1}] Avg local training loss = {sum(round_losses) / len(round_losses):.4f}")
-            n_valid = self._fedavg(failed_local)
+            n_valid = self._fedavg_finish()
             if n_valid > 0:
                 self.nan_stats["total_updates"] += 1
             else:
@@ -440,16 +538,16 @@ class MaPLeFederated(TrainerX):
         self.finalize_training()
 
     def _fedavg(self, failed_local) -> int:
-        """check_weights_valid + safe_average_weights + broadcast, on the device (federated.py)."""
+        """check_weights_valid + safe_average_weights + broadcast, on the device (federated.py), for
+        clients that finished training: pack every local client, exchange, unpack."""
         for c, fed in zip(self.clients, self.fed):
-            fed.start(collective=False)
-            if c.client_id in failed_local:
-                fed.flag.fill_(1)
-                fed.k.fedavg_pack(c.engine.flat16, c.engine.flat32, fed.flag, fed.buf)
-        if self.distributed:
-            dist.all_reduce(self.fed[0].buf, op=dist.ReduceOp.SUM)
-        else:
-            reduce_local(self.fed)
+            fed.start(collective=self.distributed, failed=c.client_id in failed_local)
+        return self._fedavg_finish()
+
+    def _fedavg_finish(self) -> int:
+        """Wait for the exchange every local client started (FedAvgBucket.start), reduce, unpack."""
+        if not self.distributed:
+            reduce_local(self.fed)  # sequential clients in one process: their buckets summed in client order
         for fed in self.fed:
             fed.finish()
         return self.fed[0].n_valid()
@@ -528,6 +626,8 @@ class MaPLeFederated(TrainerX):
         print(f"Loaded aggregator weights from '{path}' (epoch={ckpt.get('epoch')}).")
         if self.check_weights_valid(self.global_weights):
             self.broadcast_weights(self.global_weights)
+            for fed in getattr(self, "fed", []):
+                fed.snapshot()  # an all-failed round now reverts to the loaded weights
             print("Broadcasted loaded global weights.")
         else:
             print("Warning: loaded global weights invalid! Skipping broadcast.")

@@ -158,7 +158,8 @@ int mf_optim_chunk_bytes(void);
 int mf_optim_chunk_elems(void);
 int mf_clip_grad_norm(const void* g16, const float* g32, const void* chunks, int nchunks, float max_norm,
                       float* part, float* out, void* stream);
-/* coef: the clip output (coef at [1]); hyper (device): {lr, momentum, weight_decay, first_step}   */
+/* coef: the clip output (coef at [1]); hyper (device): {lr, momentum, weight_decay, first_step,    */
+/* halt}; halt != 0 skips the update (a non-finite loss, trainers/maple.py:375-376)               */
 int mf_sgd_step(void* p, void* g, void* buf, int64_t n, int is16, const float* coef, const float* hyper,
                 void* stream);
 /* bucket[0:n16+n32] = this client's trainables as fp32 (0 if *invalid_flag), bucket[n16+n32] = its vote
@@ -170,6 +171,11 @@ int mf_fedavg_pack(const void* p16, int64_t n16, const float* p32, int64_t n32, 
                    float* bucket, void* stream);
 int mf_fedavg_unpack(const float* bucket, void* p16, int64_t n16, float* p32, int64_t n32, void* g16, float* g32,
                      void* stream);
+/* FedAvg in client order (trainers/maple_fed.py:311-314: torch.stack over the clients, then mean):   */
+/* out[i] = sum_c gathered[c * stride + i] accumulated c = 0, 1, ... in fp32, for i < n; gathered    */
+/* holds every client's packed bucket (an all-gather of mf_fedavg_pack outputs)                      */
+int mf_fedavg_reduce_ordered(const float* gathered, int nclients, int64_t stride, int64_t n, float* out,
+                             void* stream);
 int mf_nonfinite_flag(const void* x, int64_t n, int is16, int* flag, void* stream);
 
 /* ---- image transforms (data step before the path) ---------------------

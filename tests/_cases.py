@@ -1,0 +1,73 @@
+"""The reference-generated parity fixtures (tests/golden/case_*.npz, made by tests/golden/make_golden.py
+in the build container by importing the reference's own clip/model.py + trainers/maple.py).
+
+Each case holds the inputs' regeneration keys (seed, client, step, J, K, B; the portable PRNG of
+federated_multi_modal_amd/synthetic.py rebuilds weights and images bit-identically on any host) and
+the reference's outputs: eval logits, train loss, tower features, and per case optionally every
+trainable gradient + the clip/SGD parameter deltas and per-block activation samples of both towers,
+each next to the float64 restatement's value (the noise floor)."""
+from __future__ import annotations
+
+from pathlib import Path
+from typing import Dict, List
+
+import numpy as np
+
+from federated_multi_modal_amd import synthetic as syn
+
+GOLD = Path(__file__).resolve().parent / "golden"
+TRACE_SAMPLE = 2048
+
+
+def case_names() -> List[str]:
+    return sorted(p.stem[len("case_"):] for p in GOLD.glob("case_*.npz"))
+
+
+def load_case(name: str) -> Dict[str, np.ndarray]:
+    return dict(np.load(GOLD / f"case_{name}.npz"))
+
+
+def case_inputs(c: Dict[str, np.ndarray]):
+    """(J, K, B, seed, classnames, ClientBatch) of a case."""
+    J, K, B, seed = int(c["J"]), int(c["K"]), int(c["B"]), int(c["seed"])
+    names = syn.synthetic_classnames(K, seed)
+    batch = syn.client_batch(seed, int(c["client"]), int(c["step"]), B, K)
+    return J, K, B, seed, names, batch
+
+
+def trace_idx(case: str, key: str, n: int) -> np.ndarray:
+    """Sample positions (flat NLD index) of one traced activation."""
+    u = syn.uniform(4321, f"trace/{case}/{key}", TRACE_SAMPLE)
+    return np.unique((u * n).astype(np.int64))
+
+
+def trace_keys(c: Dict[str, np.ndarray]) -> List[str]:
+    keys = {k[len("trace/"):-len("/val")] for k in c if k.startswith("trace/") and k.endswith("/val")}
+    return sorted(keys, key=lambda k: (k.split("/")[0], int(k.split("/")[1])))
+
+
+def sel(g, prefix, name, full):
+    """(ours, reference) for a packed tensor: full when small, else the fixture's sampled entries."""
+    if f"{prefix}full/{name}" in g:
+        return full, g[f"{prefix}full/{name}"].astype(np.float64)
+    idx = g[f"{prefix}idx/{name}"]
+    return full[idx], g[f"{prefix}val/{name}"].astype(np.float64)
+
+
+def logit_gate(ours: np.ndarray, ref: np.ndarray, ref64: np.ndarray, margin: float = 4e-3):
+    """The GPU logit gate: max|d| <= 4e-3, mean|d| <= 1.5e-3, distance to the float64
+    restatement <= 1.25x the reference's own, argmax identical on every row whose top-2 margin (in the
+    reference) exceeds `margin`.  Returns (ok, report dict)."""
+    ours = ours.astype(np.float64)
+    ref = ref.astype(np.float64)
+    err = np.abs(ours - ref)
+    e64_ours = float(np.abs(ours - ref64).max())
+    e64_ref = float(np.abs(ref - ref64).max())
+    top2 = np.sort(ref, 1)[:, -2:]
+    clear = (top2[:, 1] - top2[:, 0]) > margin
+    argmax_ok = bool(np.array_equal(ours.argmax(1)[clear], ref.argmax(1)[clear]))
+    rep = dict(max=float(err.max()), mean=float(err.mean()), e64_ours=e64_ours, e64_ref=e64_ref,
+               rows=int(ref.shape[0]), rows_compared=int(clear.sum()), argmax_ok=argmax_ok,
+               argmax_all_equal=bool(np.array_equal(ours.argmax(1), ref.argmax(1))))
+    ok = err.max() <= 4e-3 and err.mean() <= 1.5e-3 and e64_ours <= 1.25 * e64_ref and argmax_ok
+    return ok, rep

@@ -30,7 +30,9 @@ HERE = Path(__file__).resolve().parent
 sys.path.insert(0, str(HERE))
 sys.path.insert(0, str(HERE.parents[1]))
 
+sys.path.insert(0, str(HERE.parent))
 import ref_harness as h  # noqa: E402
+from _cases import trace_idx  # noqa: E402  (the GPU tests regenerate the same sample positions)
 from federated_multi_modal_amd import synthetic as syn  # noqa: E402
 from oracle import maple_oracle as O  # noqa: E402
 
@@ -124,6 +126,156 @@ def make_fedavg(seed=0):
     print("wrote fedavg.npz")
 
 
+# (name, seed, client, step, J, K, B, grads+deltas, per-layer trace) -- SURVEY.md §8(c) items 1-5
+CASES = [
+    ("c1_s0_b0", 0, 0, 0, 3, 10, 4, False, True),
+    ("c1_s0_b1", 0, 0, 1, 3, 10, 4, False, False),
+    ("c1_s1_b0", 1, 0, 0, 3, 10, 4, False, False),
+    ("c1_s1_b1", 1, 0, 1, 3, 10, 4, True, False),
+    ("c1_s2_b0", 2, 0, 0, 3, 10, 4, False, False),
+    ("c1_s2_b1", 2, 0, 1, 3, 10, 4, False, False),
+    # C3 per-client shape (BASELINE configs[2]: EuroSAT 10 classes, J=9 train.py:113, batch 4)
+    ("c3_j9_k10_b4", 0, 1, 0, 9, 10, 4, True, True),
+    ("j9_k38_b4", 5, 1, 0, 9, 38, 4, False, False),
+]
+
+
+def _hook_reference(ref, trace: dict):
+    """Forward hooks on every residual block of both towers (clip/model.py:307-352): block i's output
+    x (LND) is recorded as NLD, the layout the engine keeps in HBM."""
+    hooks = []
+    towers = (("vision", ref.image_encoder.transformer.resblocks), ("text", ref.text_encoder.transformer.resblocks))
+    for tower, blocks in towers:
+        for i, blk in enumerate(blocks):
+            def hook(mod, inp, out, key=f"{tower}/{i}"):
+                trace[key] = out[0].detach().permute(1, 0, 2).contiguous()
+            hooks.append(blk.register_forward_hook(hook))
+    return hooks
+
+
+def make_case(name, seed, client, step, J, K, B, grads, traced, lr=0.0026):
+    names = syn.synthetic_classnames(K, seed)
+    batch = syn.client_batch(seed, client, step, B, K)
+    img = torch.from_numpy(batch.images)
+    lab = torch.from_numpy(batch.labels)
+    t0 = time.time()
+    ref = h.build_reference_model(seed, J, names)
+    out = {"seed": np.array(seed), "client": np.array(client), "step": np.array(step), "J": np.array(J),
+           "K": np.array(K), "B": np.array(B), "lr": np.array(lr), "labels": batch.labels}
+    trace: dict = {}
+    hooks = _hook_reference(ref, trace) if traced else []
+    feats = {}
+    fh = [ref.image_encoder.register_forward_hook(lambda m, i, o: feats.__setitem__("img", o.detach())),
+          ref.text_encoder.register_forward_hook(lambda m, i, o: feats.__setitem__("txt", o.detach()))]
+    ref.eval()
+    with torch.no_grad():
+        out["logits"] = ref(img).numpy()
+    for hk in hooks + fh:
+        hk.remove()
+    out["img_feat"] = feats["img"].float().numpy()
+    out["txt_feat"] = feats["txt"].float().numpy()
+    ref.train()
+    if grads:
+        loss = ref(img, lab)
+        loss.backward()
+        tr = {n: p for n, p in ref.named_parameters() if p.requires_grad}
+        pack_tensors("grad/", {n: p.grad for n, p in tr.items() if p.grad is not None}, out)
+        before = {n: p.detach().clone() for n, p in tr.items()}
+        total = torch.nn.utils.clip_grad_norm_(list(tr.values()), max_norm=1.0, error_if_nonfinite=False)
+        out["total_norm"] = np.array(float(total))
+        opt = torch.optim.SGD([p for p in ref.parameters() if p.requires_grad], lr=lr, momentum=0.9,
+                              weight_decay=5e-4, dampening=0, nesterov=False)
+        opt.step()
+        pack_tensors("delta/", {n: (p.detach().double() - before[n].double()) for n, p in tr.items()
+                                if p.grad is not None}, out)
+    else:
+        with torch.no_grad():
+            loss = ref(img, lab)
+    out["loss"] = np.array(loss.item(), dtype=np.float32)
+    t_ref = time.time() - t0
+
+    # float64 restatement: the noise floor per fixture (and per layer when traced)
+    M64 = O.build_model(seed, J, names, compute_dtype=torch.float64)
+    tr64: dict = {}
+    with torch.no_grad():
+        out["logits64"] = O.forward(M64, img.double(), train=False, trace=tr64).numpy()
+    out["img_feat64"] = tr64["img_feat"].numpy()
+    out["txt_feat64"] = tr64["txt_feat"].numpy()
+    if grads:
+        loss64 = O.forward(M64, img.double(), lab, train=True)
+        loss64.backward()
+        pack_tensors("grad64/", {n: p.grad for n, p in M64.trainable().items() if p.grad is not None}, out)
+    else:
+        with torch.no_grad():
+            loss64 = O.forward(M64, img.double(), lab, train=True)
+    out["loss64"] = np.array(loss64.item())
+    if traced:
+        for key, x in trace.items():
+            flat = x.double().reshape(-1).numpy()
+            f64 = tr64[key].reshape(-1).numpy()
+            idx = trace_idx(name, key, flat.size)
+            out[f"trace/{key}/shape"] = np.array(x.shape)
+            out[f"trace/{key}/norm"] = np.array(np.linalg.norm(flat))
+            out[f"trace/{key}/norm64"] = np.array(np.linalg.norm(f64))
+            out[f"trace/{key}/err64"] = np.array(np.linalg.norm(flat - f64))  # the reference's own fp16 error
+            out[f"trace/{key}/val"] = flat[idx].astype(np.float32)
+            out[f"trace/{key}/val64"] = f64[idx]
+    np.savez_compressed(HERE / f"case_{name}.npz", **out)
+    d = np.abs(out["logits"].astype(np.float64) - out["logits64"]).max()
+    print(f"case {name}: J={J} K={K} B={B} ref {t_ref:.1f}s total {time.time() - t0:.1f}s loss {out['loss']:.5f} "
+          f"fp16-vs-fp64 logits {d:.2e}")
+
+
+def make_c5_text(seed=0, J=9, K=1000, B=2):
+    """BASELINE configs[4] text side: all 1000 class prompts (77 tokens each) through the reference's
+    TextEncoder (trainers/maple.py:52-79) and CustomCLIP's eval logits on B images."""
+    names = syn.synthetic_classnames(K, seed)
+    batch = syn.client_batch(seed, 0, 0, B, K)
+    img = torch.from_numpy(batch.images)
+    t0 = time.time()
+    ref = h.build_reference_model(seed, J, names)
+    feats = {}
+    fh = ref.text_encoder.register_forward_hook(lambda m, i, o: feats.__setitem__("txt", o.detach()))
+    ref.eval()
+    with torch.no_grad():
+        logits = ref(img).numpy()
+    fh.remove()
+    t_ref = time.time() - t0
+    M64 = O.build_model(seed, J, names, compute_dtype=torch.float64)
+    with torch.no_grad():
+        logits64 = O.forward(M64, img.double(), train=False).numpy()
+    np.savez_compressed(HERE / "case_c5_text_k1000.npz", seed=np.array(seed), client=np.array(0), step=np.array(0),
+                        J=np.array(J), K=np.array(K), B=np.array(B), labels=batch.labels, logits=logits,
+                        logits64=logits64, txt_feat=feats["txt"].numpy())
+    d = np.abs(logits.astype(np.float64) - logits64).max()
+    print(f"case c5_text_k1000: ref {t_ref:.1f}s total {time.time() - t0:.1f}s fp16-vs-fp64 logits {d:.2e}")
+
+
+def make_state_dict_keys():
+    """The reference CustomCLIP.state_dict() key set, shapes and dtypes (trainers/maple.py:221-229) at
+    J=3 and J=9, and the dtypes FedAvg leaves in the aggregator checkpoint (every key .half(),
+    trainers/maple_fed.py:314, 367-386)."""
+    import json
+    out = {}
+    for J in (3, 9):
+        ref = h.build_reference_model(0, J, syn.synthetic_classnames(10, 0))
+        sd = ref.state_dict()
+        out[f"J{J}"] = [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in sd.items()]
+    (HERE / "state_dict_keys.json").write_text(json.dumps(out, indent=0))
+    print("wrote state_dict_keys.json:", {k: len(v) for k, v in out.items()})
+
+
 if __name__ == "__main__":
-    make_fedavg()
-    make_c1()
+    import sys as _sys
+    what = _sys.argv[1:] or ["fedavg", "c1", "cases", "c5", "keys"]
+    if "fedavg" in what:
+        make_fedavg()
+    if "c1" in what:
+        make_c1()
+    if "cases" in what:
+        for c in CASES:
+            make_case(*c)
+    if "c5" in what:
+        make_c5_text()
+    if "keys" in what:
+        make_state_dict_keys()

@@ -138,7 +138,7 @@ def test_engine_vs_oracle_other_shape(dev):
     print(f"J=9 K=38 B=3 logits max|err| {err.max():.3e} mean {err.mean():.3e}")
     assert err.mean() <= 1.5e-3 and err.max() <= 4e-3
     top2 = np.sort(ref, 1)[:, -2:]
-    clear = (top2[:, 1] - top2[:, 0]) > 8e-3  # argmax is only defined past the tolerance
+    clear = (top2[:, 1] - top2[:, 0]) > 4e-3  # argmax is only defined past the tolerance
     assert np.array_equal(logits.argmax(1)[clear], ref.argmax(1)[clear])
 
 
@@ -269,3 +269,44 @@ def test_c4_full_size_properties(dev):
     full2 = e0.forward().clone()
     cached2 = e0.forward(reuse_text=True).clone()
     assert torch.equal(full2, cached2) and not torch.equal(full, full2)
+
+
+def test_c5_full_size_properties(dev):
+    """BASELINE configs[4] size (B=32, K=1000 class prompts of 77 tokens, J=9): the text tower runs
+    77 000 rows (M of every text GEMM) and 8 000 causal attention heads.  The reference's own outputs on
+    all 1000 prompts are pinned at B=2 (tests/golden/case_c5_text_k1000.npz, test_parity_cases_gpu.py);
+    here, size-independent properties at the full size: two engines from one seed agree bit for bit
+    (logits, loss, every gradient, updated weights), the EOT-truncated tower gives bit-identical logits
+    and loss, cached-text eval equals a full forward, everything finite."""
+    J, K, B, seed = 9, 1000, 32, 0
+    names = syn.synthetic_classnames(K, seed)
+    b = syn.client_batch(seed, 0, 0, B, K)
+    runs = []
+    for trunc in (False, False, True):
+        e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed, eot_truncate=trunc),
+                        device=dev)
+        e.set_lr(0.0026)
+        e.load_batch(torch.from_numpy(b.images), torch.from_numpy(b.labels))
+        logits = e.forward().clone()
+        e.forward_backward()
+        loss = e.loss()
+        if trunc:
+            runs.append((logits, loss, None, None))
+            del e
+            break
+        grads = {k: v.detach().clone() for k, v in e.grads().items()}
+        e.optimizer_step()
+        params = {k: v.detach().clone() for k, v in e.trainable_state().items()}
+        runs.append((logits, loss, grads, params))
+        if len(runs) == 2:
+            full = e.forward().clone()
+            cached = e.forward(reuse_text=True).clone()
+            assert torch.equal(full, cached)
+        del e
+        torch.cuda.empty_cache()
+    (l0, s0, g0, p0), (l1, s1, g1, p1), (l2, s2, _, _) = runs
+    assert torch.isfinite(l0.float()).all() and np.isfinite(s0)
+    assert torch.equal(l0, l1) and s0 == s1
+    assert all(torch.equal(g0[k], g1[k]) for k in g0) and all(torch.equal(p0[k], p1[k]) for k in p0)
+    assert all(torch.isfinite(v.float()).all() for v in g0.values())
+    assert torch.equal(l0, l2) and s0 == s2

@@ -1,10 +1,11 @@
-"""CPU tier: the FedAvg collective protocol (federated_multi_modal_amd/federated.py) across
-world_size 2 and 3 gloo ranks, one client per rank, checked against the reference's
-safe_average_weights / check_weights_valid semantics (trainers/maple_fed.py:271-325, restated in
-oracle/maple_oracle.py and pinned to the reference by tests/golden/fedavg.npz).
+"""CPU tier: the FedAvg collective protocol (federated_multi_modal_amd/federated.py) and the federated
+round loop (trainers.MaPLeFederated.train) across world_size 2 and 3 gloo ranks, one client per rank,
+checked against the reference's safe_average_weights / check_weights_valid semantics
+(trainers/maple_fed.py:228-325, restated in oracle/maple_oracle.py and pinned to the reference by
+tests/golden/fedavg.npz).
 
 The device kernels are replaced by host restatements here (no GPU in this tier); the GPU tier
-(tests/test_kernels_gpu.py) checks the kernels themselves."""
+(tests/test_kernels_gpu.py) checks the kernels themselves against the same restatements."""
 import os
 import socket
 
@@ -32,6 +33,14 @@ class HostKernels:
         bucket[n16 + n32] = 0.0 if bad else 1.0
 
     @staticmethod
+    def fedavg_reduce_ordered(gathered, nclients, out):
+        g = gathered.view(nclients, -1)[:, :out.numel()]
+        acc = g[0].clone()
+        for c in range(1, nclients):
+            acc += g[c]
+        out.copy_(acc)
+
+    @staticmethod
     def fedavg_unpack(bucket, p16, p32, g16, g32):
         n16, n32 = p16.numel(), p32.numel()
         n_valid = float(bucket[n16 + n32])
@@ -47,18 +56,26 @@ class HostKernels:
 
 
 class FakeEngine:
-    def __init__(self, rank, n16=37, n32=29, bad=False):
+    """flat16/flat32 trainables of one client; fp32 values spread over several binades so the fp32
+    summation order of three clients shows in the fp16-rounded mean (~60 of the 1M elements differ
+    between client order and a rotated order)."""
+
+    def __init__(self, rank, n16=37, n32=(1 << 20) + 3, bad=False):
         g = torch.Generator().manual_seed(100 + rank)
         self.device = torch.device("cpu")
         self.n16, self.n32 = n16, n32
         self.flat16 = torch.randn(n16, generator=g).half()
-        self.flat32 = torch.randn(n32, generator=g)
+        self.flat32 = torch.randn(n32, generator=g) * torch.exp2(torch.randint(-6, 6, (n32,), generator=g).float())
         if bad:
             self.flat32[3] = float("nan")
         self.reloaded = 0
+        self.momentum_resets = 0
 
     def after_weights_loaded(self):
         self.reloaded += 1
+
+    def reset_momentum(self):
+        self.momentum_resets += 1
 
 
 def _free_port():
@@ -69,15 +86,19 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, bad_ranks, out):
+def _init(rank, world, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _worker(rank, world, port, bad_ranks, mode, out):
+    _init(rank, world, port)
     from federated_multi_modal_amd.federated import FedAvgBucket
     e = FakeEngine(rank, bad=rank in bad_ranks)
     g16, g32 = e.flat16.clone(), e.flat32.clone()
     e.flat16.copy_(FakeEngine(0).flat16)  # the previous global weights (identical on every rank)
     e.flat32.copy_(FakeEngine(0).flat32)
-    fed = FedAvgBucket(e, kernels=HostKernels)
+    fed = FedAvgBucket(e, kernels=HostKernels, mode=mode)
     e.flat16.copy_(g16)  # ... then this client's local training result
     e.flat32.copy_(g32)
     n_valid = fed.run()
@@ -85,28 +106,150 @@ def _worker(rank, world, port, bad_ranks, out):
     dist.destroy_process_group()
 
 
-def _run(world, bad_ranks=()):
+def _spawn(fn, world, *args):
     port = _free_port()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, port, tuple(bad_ranks), out), nprocs=world, join=True)
+    mp.spawn(fn, args=(world, port) + args + (out,), nprocs=world, join=True)
     return dict(out)
 
 
-@pytest.mark.parametrize("world,bad", [(2, ()), (3, (1,)), (2, (0, 1))])
-def test_fedavg_allreduce_matches_reference(world, bad):
-    res = _run(world, bad)
+@pytest.mark.parametrize("world,bad,mode", [(2, (), "ordered"), (3, (), "ordered"), (3, (1,), "ordered"),
+                                            (2, (0, 1), "ordered"), (3, (), "allreduce"), (2, (1,), "allreduce")])
+def test_fedavg_exchange_matches_reference(world, bad, mode):
+    res = _spawn(_worker, world, tuple(bad), mode)
     clients = [FakeEngine(r, bad=r in bad) for r in range(world)]
     valid = [c for c in clients if O.check_weights_valid({"a": c.flat16, "b": c.flat32})]
     for r in range(world):
         n_valid, p16, p32, reloaded = res[r]
         assert n_valid == len(valid)
+        assert reloaded == 1
         if not valid:  # all clients failed: round skipped, every client back to the previous global
             assert torch.equal(p16, FakeEngine(0).flat16) and torch.equal(p32, FakeEngine(0).flat32)
             continue
         ref = O.safe_average_weights([{"a": c.flat16, "b": c.flat32} for c in valid])
-        assert torch.equal(p16, ref["a"])                      # fp16 keys: bit-exact
-        assert torch.equal(p32, ref["b"].float())              # fp32 keys take the .half() rounding
-        assert reloaded == 1
-    # every rank holds the same global weights (broadcast-free all-reduce)
-    assert all(torch.equal(res[0][1], res[r][1]) for r in range(world))
+        if mode == "ordered":  # client-order fp32 sums: bit-exact at any world size
+            assert torch.equal(p16, ref["a"])
+            assert torch.equal(p32, ref["b"].float())
+        else:  # collective order: within one fp16 ulp
+            ulp = torch.exp2(torch.floor(torch.log2(ref["b"].float().abs().clamp_min(2.0 ** -14))) - 10)
+            assert ((p32 - ref["b"].float()).abs() <= ulp).all()
+            assert torch.equal(p16, ref["a"]) or world > 2
+    # every rank holds the same global weights (broadcast-free exchange)
+    assert all(torch.equal(res[0][1], res[r][1]) and torch.equal(res[0][2], res[r][2]) for r in range(world))
+
+
+# ----------------------------------------------------------------------------- the round loop itself
+
+class _Optim:
+    def __init__(self):
+        self.lr = 1e-3
+        self.sched = None
+
+    def rebuild(self, epoch):
+        pass
+
+
+class FakeClient:
+    """Stands in for MaPLe (one client per rank) in MaPLeFederated.train(): run_epoch "trains" by a
+    deterministic per-(client, round, epoch) update, fails with the reference's RuntimeError when told,
+    calls before_test exactly where MaPLe.run_epoch does, and logs the order of events."""
+
+    def __init__(self, rank, fail_rounds=()):
+        self.client_id = rank
+        self.engine = FakeEngine(0)  # every client starts from the same global weights
+        self.optim = _Optim()
+        self.sched = None
+        self.fail_rounds = set(fail_rounds)
+        self.events = []
+        self.model = self
+
+    def state_dict(self):
+        return {"flat16": self.engine.flat16, "flat32": self.engine.flat32}
+
+    @staticmethod
+    def local_update(rank, round_idx, ep, e):
+        g = torch.Generator().manual_seed(1000 * rank + 100 * round_idx + ep)
+        e.flat16 += (1e-2 * torch.randn(e.n16, generator=g)).half()
+        e.flat32 += 1e-3 * torch.randn(e.n32, generator=g) * e.flat32.abs()
+
+    def run_epoch(self, ep, before_test=None):
+        round_idx = ep // 2
+        if round_idx in self.fail_rounds and ep % 2 == 1:
+            self.events.append(("fail", ep))
+            raise RuntimeError("NaN/Inf in total loss")
+        self.local_update(self.client_id, round_idx, ep, self.engine)
+        if before_test is not None:
+            self.events.append(("fedavg_start", ep))
+            before_test()
+        self.events.append(("test", ep))
+        return {"avg_loss": 1.0}
+
+    def test(self, evaluate_train=False):
+        self.events.append(("global_test", None))
+        return {"accuracy": 50.0}
+
+
+def _train_worker(rank, world, port, fail, out):
+    _init(rank, world, port)
+    from federated_multi_modal_amd.config import extend_cfg, get_cfg_default
+    from federated_multi_modal_amd.federated import FedAvgBucket
+    from federated_multi_modal_amd.trainers import MaPLeFederated
+    cfg = get_cfg_default()
+    extend_cfg(cfg)
+    cfg.OUTPUT_DIR = f"/tmp/mapfed_fedtest_{port}"
+    tr = MaPLeFederated.__new__(MaPLeFederated)   # the round loop without building GPU engines
+    tr.cfg, tr.num_clients, tr.num_rounds, tr.local_epochs = cfg, world, 2, 2
+    tr.nan_stats = {"total_updates": 0, "failed_clients": [], "skipped_rounds": 0}
+    tr.distributed, tr.rank = True, rank
+    client = FakeClient(rank, fail_rounds=fail.get(rank, ()))
+    tr.clients = [client]
+    tr.fed = [FedAvgBucket(client.engine, kernels=HostKernels, mode="ordered")]
+    tr.save_model = lambda *a, **k: None
+    tr.train()
+    out[rank] = (client.engine.flat16.clone(), client.engine.flat32.clone(), list(client.events), dict(tr.nan_stats),
+                 client.engine.momentum_resets)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail", [(2, {}), (3, {1: (0,)}), (2, {0: (1,), 1: (1,)})])
+def test_round_loop_distributed(world, fail):
+    """MaPLeFederated.train() on gloo ranks: 2 rounds x 2 local epochs; each client's FedAvg exchange starts
+    inside its last local epoch, after the SGD steps and before that epoch's test() (the overlap), and the
+    global weights after every round equal safe_average_weights over the clients that did not fail,
+    bit for bit; an all-failed round keeps the previous global weights (trainers/maple_fed.py:262-303)."""
+    res = _spawn(_train_worker, world, fail)
+    # expected: replay the rounds on the host with the reference's aggregation
+    g16, g32 = FakeEngine(0).flat16.clone(), FakeEngine(0).flat32.clone()
+    for r in range(2):
+        locals_ = []
+        for c in range(world):
+            e = FakeEngine(0)
+            e.flat16.copy_(g16)
+            e.flat32.copy_(g32)
+            failed = r in fail.get(c, ())
+            for ep in (2 * r, 2 * r + 1):
+                if failed and ep % 2 == 1:
+                    break
+                FakeClient.local_update(c, r, ep, e)
+            if not failed:
+                locals_.append({"a": e.flat16, "b": e.flat32})
+        if locals_:
+            avg = O.safe_average_weights(locals_)
+            g16, g32 = avg["a"], avg["b"].float()
+    for rank in range(world):
+        p16, p32, events, stats, resets = res[rank]
+        assert torch.equal(p16, g16) and torch.equal(p32, g32), rank
+        assert resets == 2  # broadcast_weights drops the SGD momentum every round
+        for r in range(2):
+            if r in fail.get(rank, ()):
+                assert ("fail", 2 * r + 1) in events
+                continue
+            i = events.index(("fedavg_start", 2 * r + 1))
+            assert events[i + 1] == ("test", 2 * r + 1)      # the exchange overlaps the last local test
+            assert ("fedavg_start", 2 * r) not in events       # started once per round, in the last epoch
+    n_failed = sum(len(v) for v in fail.values())
+    assert res[0][3]["failed_clients"].__len__() == len(fail.get(0, ()))
+    skipped = sum(1 for r in range(2) if all(r in fail.get(c, ()) for c in range(world)))
+    assert res[0][3]["skipped_rounds"] == skipped and res[0][3]["total_updates"] == 2 - skipped
+    assert n_failed >= 0

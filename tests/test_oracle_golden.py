@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 import torch
 
+import _cases as C
 from federated_multi_modal_amd import synthetic as syn
 from oracle import maple_oracle as O
 
@@ -54,13 +55,12 @@ def test_golden_inputs_regenerate(c1):
 
 
 def test_oracle_logits_match_reference(c1, c1_oracle):
-    """Oracle eval logits == the reference's (trainers/maple.py:304-346) on the same inputs."""
-    ours = c1_oracle["logits"].float().numpy()
-    ref = c1["logits"].astype(np.float32)
-    assert np.abs(ours - ref).max() <= 1e-3
-    assert np.array_equal(ours.argmax(1), ref.argmax(1))
+    """Oracle eval logits == the reference's (trainers/maple.py:304-346) on the same inputs, bit for bit."""
+    ours = c1_oracle["logits"].numpy()
+    assert ours.dtype == np.float16
+    assert np.array_equal(ours, c1["logits"])
     # the fp16 noise floor the 1e-3 gate sits on (SURVEY.md §7): fp16-vs-fp64 gap of the reference
-    assert np.abs(ref - c1["logits64"]).max() < 5e-3
+    assert np.abs(c1["logits"].astype(np.float64) - c1["logits64"]).max() < 5e-3
 
 
 def test_oracle_loss_and_grads_match_reference(c1, c1_oracle):
@@ -89,6 +89,35 @@ def test_oracle_sgd_deltas_match_reference(c1, c1_oracle):
         got = got if idx is None else got[idx]
         scale = np.abs(val).max() + 1e-12
         assert np.abs(got - val).max() <= 2e-2 * scale + 1e-6, k
+
+
+@pytest.mark.parametrize("name", C.case_names())
+def test_oracle_matches_reference_case(name):
+    """Every reference-generated fixture (tests/golden/case_*.npz: C1 at 3 seeds x 2 batches, the C3
+    per-client shape J=9 K=10 B=4, J=9 K=38 B=4, the C5 text side K=1000): the oracle's fp16 eval
+    logits, tower features and train loss equal the reference's bit for bit; on traced cases every
+    block output of both towers (clip/model.py:307-352) too."""
+    c = C.load_case(name)
+    J, K, B, seed, names, batch = C.case_inputs(c)
+    M = O.build_model(seed, J, names)
+    img = torch.from_numpy(batch.images)
+    tr: dict = {}
+    with torch.no_grad():
+        logits = O.forward(M, img, train=False, trace=tr).numpy()
+    assert np.array_equal(logits, c["logits"])
+    assert np.array_equal(tr["txt_feat"].float().numpy(), c["txt_feat"].astype(np.float32))
+    if "img_feat" in c:
+        assert np.array_equal(tr["img_feat"].float().numpy(), c["img_feat"])
+    for key in C.trace_keys(c):
+        flat = tr[key].double().reshape(-1).numpy()
+        assert tuple(tr[key].shape) == tuple(c[f"trace/{key}/shape"]), key
+        idx = C.trace_idx(name, key, flat.size)
+        assert np.array_equal(flat[idx].astype(np.float32), c[f"trace/{key}/val"]), key
+        assert np.isclose(np.linalg.norm(flat), float(c[f"trace/{key}/norm"]), rtol=1e-12), key
+    if "loss" in c:
+        with torch.no_grad():
+            loss = O.forward(M, img, torch.from_numpy(batch.labels), train=True)
+        assert float(loss) == float(c["loss"])
 
 
 def test_oracle_fedavg_matches_reference():

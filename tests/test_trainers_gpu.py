@@ -1,25 +1,32 @@
 """GPU tier: the reference's trainer API (train.py -> build_trainer -> MaPLeFederated / MaPLe) running
 on the MI355X engine: a 2-client, 1-round federated run, FedAvg against the reference's
 safe_average_weights, the checkpoint format and the eval-only path (train.py:179-182)."""
+import json
 import os
+from pathlib import Path
 
+import numpy as np
 import pytest
 import torch
 
+from federated_multi_modal_amd import synthetic as syn
 from federated_multi_modal_amd.config import get_cfg_default, extend_cfg
 from federated_multi_modal_amd.trainers import build_trainer
+from oracle import maple_oracle as O
+
+GOLD = Path(__file__).resolve().parent / "golden"
 
 pytestmark = pytest.mark.gpu
 
 
-def small_cfg(out, clients=2, rounds=1, epochs=2):
+def small_cfg(out, clients=2, rounds=1, epochs=2, extra=()):
     cfg = get_cfg_default()
     extend_cfg(cfg)
     cfg.merge_from_file("configs/trainers/MaPLeFederated/vit_b16_c2_ep5_batch4_2ctx_cross_datasets.yaml")
     cfg.merge_from_list(["TRAINER.NAME", "MaPLeFederated", "SEED", 1, "OUTPUT_DIR", str(out),
                          "FED.NUM_CLIENTS", clients, "FED.NUM_ROUNDS", rounds, "FED.LOCAL_EPOCHS", epochs,
                          "MODEL.NUM_CLASSES", 10, "DATASET.NUM_SHOTS", 1, "DATALOADER.TEST.BATCH_SIZE", 12,
-                         "TRAINER.MAPLE.PROMPT_DEPTH", 3])
+                         "TRAINER.MAPLE.PROMPT_DEPTH", 3] + list(extra))
     cfg.freeze()
     return cfg
 
@@ -31,7 +38,8 @@ def test_federated_round_checkpoint_and_eval_only(dev, tmp_path):
     res = tr.clients[0].forward_backward(next(iter(tr.clients[0].dm.train_loader)))
     assert isinstance(res["loss"], float) and res["loss"] == res["loss"]
     assert len(tr.clients[0].grad_norms) == 1 and 0.0 < tr.clients[0].grad_norms[0] <= 1.0 + 1e-3
-    # FedAvg of two clients == the reference's safe_average_weights on their trainables (bit-exact)
+    # FedAvg of two clients == the reference's safe_average_weights (the oracle, pinned to the reference by
+    # tests/golden/fedavg.npz) on their trainables, bit-exact
     for c in tr.clients:
         c.run_epoch(0)
     names = tr.clients[0].engine.trainable_names
@@ -39,7 +47,7 @@ def test_federated_round_checkpoint_and_eval_only(dev, tmp_path):
     assert not all(torch.equal(snaps[0][n], snaps[1][n]) for n in names)
     n_valid = tr._fedavg([])
     assert n_valid == 2
-    ref = tr.safe_average_weights(snaps, 2)
+    ref = O.safe_average_weights(snaps)
     for n in names:
         for c in tr.clients:
             got = c.engine.P[n].detach().cpu()
@@ -52,7 +60,15 @@ def test_federated_round_checkpoint_and_eval_only(dev, tmp_path):
     sd = torch.load(ck, map_location="cpu", weights_only=True)
     assert sd["epoch"] == cfg.OPTIM.MAX_EPOCH and sd["optimizer"] is None
     assert all(v.dtype == torch.float16 for v in sd["state_dict"].values())
-    assert "prompt_learner.ctx" in sd["state_dict"] and any(k.startswith("clip_model2.") for k in sd["state_dict"])
+    # exactly the reference CustomCLIP.state_dict() key set and shapes at J=3 (616 keys incl. the
+    # clip_model2.* aliases and clip_model2.token_embedding.weight; tests/golden/state_dict_keys.json,
+    # generated from the reference), all fp16 as FedAvg leaves them (trainers/maple_fed.py:314)
+    gold = {k: tuple(shape) for k, shape, _ in json.loads((GOLD / "state_dict_keys.json").read_text())["J3"]}
+    assert {k: tuple(v.shape) for k, v in sd["state_dict"].items()} == {
+        k: (shape if not k.startswith("prompt_learner.token_") else (10,) + shape[1:]) for k, shape in gold.items()}
+    tok = sd["state_dict"]["clip_model2.token_embedding.weight"].float().numpy()
+    rows = [7, 49406, 12345]
+    assert np.array_equal(tok[rows], syn.token_embedding_rows(1, np.array(rows)))
     acc0 = tr.clients[0].test()["accuracy"]
     # eval-only: a fresh aggregator loads the checkpoint and reproduces the accuracy
     tr2 = build_trainer(cfg)
@@ -91,3 +107,67 @@ def test_soft_label_batches_through_the_trainer(dev, tmp_path):
     assert c.engine.soft_labels is False
     with pytest.raises(ValueError):
         c.forward_backward(dict(batch, label=soft[:, :-1].contiguous()))
+
+
+def test_reference_format_checkpoint_strict_load_and_init_weights(dev, tmp_path):
+    """A checkpoint with the reference's key set (the aggregator file written by save_model, equal to
+    tests/golden/state_dict_keys.json) loads with strict=True (trainers/maple_fed.py:330), and through
+    MODEL.INIT_WEIGHTS (Dassl load_pretrained_weights, trainers/maple.py:489-490) into a fresh client:
+    every trainable then holds the checkpoint's values."""
+    cfg = small_cfg(tmp_path, clients=1, epochs=1)
+    tr = build_trainer(cfg)
+    tr.train()
+    ck = os.path.join(str(tmp_path), "MultiModalPromptLearner_Aggregator", f"model.pth.tar-{cfg.OPTIM.MAX_EPOCH}")
+    sd = torch.load(ck, map_location="cpu", weights_only=True)["state_dict"]
+    c = tr.clients[0]
+    c.model.load_state_dict(sd, strict=True)
+    bad = dict(sd)
+    bad.pop("clip_model2.token_embedding.weight")
+    with pytest.raises(RuntimeError):
+        c.model.load_state_dict(bad, strict=True)
+    cfg2 = small_cfg(tmp_path / "b", clients=1, epochs=1, extra=["MODEL.INIT_WEIGHTS", ck, "SEED", 2])
+    tr2 = build_trainer(cfg2)
+    e2 = tr2.clients[0].engine
+    for n in e2.trainable_names:
+        assert torch.equal(e2.P[n].detach().cpu().float(), sd[n].float()), n
+    assert torch.equal(e2.P["image_encoder.conv1.weight"].cpu(), sd["image_encoder.conv1.weight"])
+
+
+def test_nonfinite_loss_stops_the_epoch_at_its_step(dev, tmp_path):
+    """trainers/maple.py:375-376 + :617-627: the first non-finite loss raises RuntimeError out of the epoch
+    with the weights as they were before that step; total_batches counts up to the failing batch.  Here
+    step 2 of 4 sees a NaN image (inside the graph-replayed epoch, no per-step host sync)."""
+    cfg = small_cfg(tmp_path, clients=1)
+    K = 10
+    batches = []
+    for s in range(4):
+        b = syn.client_batch(1, 0, s, 4, K)
+        batches.append({"img": torch.from_numpy(b.images).to(dev), "label": torch.from_numpy(b.labels).to(dev),
+                        "caption": [""] * 4})
+    batches[2]["img"][1, 0, 5, 5] = float("nan")
+
+    class DM:
+        def __init__(self, base, train):
+            self.train_loader, self.test_loader = train, base.test_loader
+
+    tr = build_trainer(cfg)
+    c = tr.clients[0]
+    c.dm = DM(c.dm, batches)
+    with pytest.raises(RuntimeError, match="NaN/Inf in total loss"):
+        c.run_epoch(0)
+    assert c.total_batches == 3 and c.batch_idx == 2
+    got = {n: v.detach().clone() for n, v in c.engine.trainable_state().items()}
+    ref_tr = build_trainer(cfg)
+    r = ref_tr.clients[0]
+    for b in batches[:2]:
+        r.forward_backward(b)
+    for n, v in r.engine.trainable_state().items():
+        assert torch.equal(got[n], v), n
+    # the per-batch API raises at the bad batch itself, and the next good batch trains again
+    with pytest.raises(RuntimeError, match="NaN/Inf in total loss"):
+        r.forward_backward(batches[2])
+    assert torch.equal(r.engine.flat16, c.engine.flat16) and torch.equal(r.engine.flat32, c.engine.flat32)
+    r.forward_backward(batches[3])
+    assert not torch.equal(r.engine.flat16, c.engine.flat16)
+    with pytest.raises(AssertionError, match="Label index out of bounds"):
+        r.forward_backward(dict(batches[3], label=batches[3]["label"].clone().fill_(K)))
