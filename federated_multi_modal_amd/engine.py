@@ -304,9 +304,10 @@ class MapleEngine:
             # copies for the reference's state-dict key set; the table is generated on first use when the
             # weights are the seeded synthetic CLIP
             self.clip_logit_scale = torch.tensor(float(vals.get("clip_model2.logit_scale", math.log(1 / 0.07))),
-                                                 dtype=F32)
+                                                 dtype=F32, device=self.device)
             tok = vals.get("clip_model2.token_embedding.weight")
             self._token_table = None if tok is None else torch.as_tensor(np.asarray(tok, dtype=np.float32))
+            self._table_owner = self
             self._build_text_constants()
             # {lr, momentum, weight_decay, first_step, halt}: read by the SGD kernels from device memory
             self.hyper = torch.tensor([0.0, cfg.momentum, cfg.weight_decay, 1.0, 0.0], device=self.device, dtype=F32)
@@ -316,7 +317,7 @@ class MapleEngine:
             for a in ("n16", "n32", "flat16", "flat32", "gflat16", "gflat32", "mom16", "mom32", "P", "G",
                       "trainable_names", "conv_w", "chunks", "nchunks", "norm_part", "clip_out", "WT", "tokenized",
                       "token_prefix", "token_suffix", "token_suffix_run", "text_len", "eot_rows", "hyper",
-                      "clip_logit_scale", "_token_table"):
+                      "clip_logit_scale", "_table_owner"):
                 setattr(self, a, getattr(shared, a))
         G2 = d.grid * d.grid
         self.Lv = G2 + 1 + cfg.n_ctx
@@ -455,6 +456,7 @@ class MapleEngine:
         # soft (float) labels [B, K] select the KL branch of the loss (trainers/maple.py:356-360)
         self.soft_label_in = torch.zeros(B, K, device=dev, dtype=F32)
         self.soft_labels = False
+        self.input_flag = torch.zeros(1, device=dev, dtype=torch.int32)
         self.im2col = e(B * self.G2, 3 * d.vision_patch ** 2)
         self.patch = e(B * self.G2, dv)
         self.Xpre = e(B * self.Lv, dv)
@@ -636,10 +638,19 @@ class MapleEngine:
                               accumulate=False, zero_rows=False)
         v.lnb.finish()
 
-    def forward_backward(self):
-        """loss = CustomCLIP(image, label); loss.backward()  — grads land in gflat16/gflat32.
-        The trainable block's W^T copies (read by its dX products) are refreshed from the current
-        weights first, on the side stream, where they overlap the vision forward."""
+    def forward_loss(self):
+        """loss = CustomCLIP(image, label) (trainers/maple.py:304-381): the forward, the loss, and d loss /
+        d features (the fused loss kernel).  The trainable block's W^T copies (read by its dX products in
+        backward()) are refreshed from the current weights first, on the side stream, where they overlap
+        the vision forward."""
+        # check_tensor_validity of the inputs (trainers/maple.py:556-557) on the device: a NaN/Inf image (or
+        # soft label) sets input_flag and halts the update like a non-finite loss; the trainer raises
+        # ValueError for it at the end of the epoch
+        self.input_flag.zero_()
+        ops.nonfinite_flag(self.img_in, self.input_flag)
+        if self.soft_labels:
+            ops.nonfinite_flag(self.soft_label_in, self.input_flag)
+        torch.maximum(self.hyper[4:5], self.input_flag.to(F32), out=self.hyper[4:5])
         main = torch.cuda.current_stream(self.device)
         side = self.side if self.overlap_towers else main
         side.wait_stream(main)
@@ -654,6 +665,9 @@ class MapleEngine:
             ops.clip_loss_fwd_bwd(self.img_feat, self.txt_feat, self.img_n, self.txt_n, self.norms, self.logits,
                                   self.label_in, self.P["logit_scale"], self.dmm, self.cos_ws, self.loss_out,
                                   self.dimg_n, self.dtxt_n, self.dimg, self.dtxt)
+
+    def backward(self):
+        """loss.backward() after forward_loss(): every trainable gradient lands in gflat16 / gflat32."""
         main = torch.cuda.current_stream(self.device)
         side = self.side if self.overlap_towers else main
         side.wait_stream(main)
@@ -662,6 +676,11 @@ class MapleEngine:
         self._vision_backward()
         main.wait_stream(side)
         self._prompt_learner_bwd()
+
+    def forward_backward(self):
+        """loss = CustomCLIP(image, label); loss.backward()  — grads land in gflat16/gflat32."""
+        self.forward_loss()
+        self.backward()
 
     # ------------------------------------------------------------------ optimizer
     def set_lr(self, lr: float):
@@ -723,13 +742,16 @@ class MapleEngine:
         return {n: t for n, t in self.P.items()}
 
     def token_embedding_table(self) -> torch.Tensor:
-        """CLIP's token-embedding table [vocab, 512] fp32 (host): the checkpoint's, or the seeded
-        synthetic one (the same values the prompt rows were taken from)."""
-        if self._token_table is None:
-            d = self.cfg.dims
-            tab = syn.fp16_round(0.02 * syn.normal(self.cfg.seed, "token_embedding.weight", d.vocab_size * d.text_width))
-            self._token_table = torch.from_numpy(tab.reshape(d.vocab_size, d.text_width))
-        return self._token_table
+        """CLIP's token-embedding table [vocab, 512] fp32 on the device (clip/model.py:642; frozen): the
+        checkpoint's, or the seeded synthetic one (the values the prompt rows were taken from)."""
+        o = self._table_owner
+        if o._token_table is None:
+            d = o.cfg.dims
+            tab = syn.fp16_round(0.02 * syn.normal(o.cfg.seed, "token_embedding.weight", d.vocab_size * d.text_width))
+            o._token_table = torch.from_numpy(tab.reshape(d.vocab_size, d.text_width))
+        if o._token_table.device != o.device:
+            o._token_table = o._token_table.to(o.device)
+        return o._token_table
 
     @staticmethod
     def alias_of(name: str) -> Optional[str]:
@@ -777,9 +799,9 @@ class MapleEngine:
                     t.copy_(torch.as_tensor(src).reshape(t.shape).to(device=t.device, dtype=t.dtype))
                     frozen_changed |= n not in self.trainable_names
             if "clip_model2.logit_scale" in sd:
-                self.clip_logit_scale.copy_(torch.as_tensor(sd["clip_model2.logit_scale"]).float().cpu())
+                self.clip_logit_scale.copy_(torch.as_tensor(sd["clip_model2.logit_scale"]).float())
             if "clip_model2.token_embedding.weight" in sd:
-                self._token_table = torch.as_tensor(sd["clip_model2.token_embedding.weight"]).float().cpu().clone()
+                self.token_embedding_table().copy_(torch.as_tensor(sd["clip_model2.token_embedding.weight"]).float())
             if "prompt_learner.token_prefix" in sd:
                 self.token_prefix.copy_(sd["prompt_learner.token_prefix"])
                 self.token_suffix.copy_(sd["prompt_learner.token_suffix"])

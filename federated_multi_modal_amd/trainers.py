@@ -31,6 +31,7 @@ from . import ops
 from .data import DATASET_CLASSES, SyntheticClientDataManager, unified_classnames
 from .engine import EngineConfig, MapleEngine
 from .federated import FedAvgBucket, reduce_local
+from .modules import CustomCLIP
 from .schedule import HostLR
 
 
@@ -109,31 +110,6 @@ class TrainerX:
         return names_real
 
 
-class _ModelView:
-    """The `model` attribute of a client (CustomCLIP stand-in): state_dict / load_state_dict /
-    train / eval / parameters counts, backed by the engine's device tensors."""
-
-    def __init__(self, engine: MapleEngine):
-        self.e = engine
-        self.training = True
-
-    def state_dict(self):
-        return self.e.reference_state_dict()
-
-    def load_state_dict(self, sd, strict: bool = True):
-        self.e.load_state_dict(sd, strict=strict)
-
-    def train(self, mode: bool = True):
-        self.training = mode
-        return self
-
-    def eval(self):
-        return self.train(False)
-
-    def trainable_parameters(self):
-        return self.e.trainable_state()
-
-
 @TRAINER_REGISTRY.register()
 class MaPLe(TrainerX):
     """One federated client (trainers/maple.py:384-716) on one GPU."""
@@ -192,7 +168,7 @@ class MaPLe(TrainerX):
             raise NotImplementedError(f"optimizer {cfg.OPTIM.NAME}: the MaPLe configs use sgd")
         self.engine = MapleEngine(ecfg, device=self.device, state=state)
         self._eval_engine: Optional[MapleEngine] = None
-        self.model = _ModelView(self.engine)
+        self.model = CustomCLIP(self.engine)  # the reference's module API over the engine (modules.py)
         if cfg.MODEL.INIT_WEIGHTS:
             load_pretrained_weights(self.model, cfg.MODEL.INIT_WEIGHTS)
         self.optim = HostLR(cfg.OPTIM)          # param_groups[0]['lr'] and the scheduler
@@ -203,6 +179,8 @@ class MaPLe(TrainerX):
         self._loss_sum = torch.zeros(1, device=self.device)
         self._bad = torch.zeros(1, device=self.device)
         self._ok = torch.zeros(1, device=self.device)   # steps of the epoch before its first non-finite loss
+        self._bad_in = torch.zeros(1, device=self.device)  # the same for non-finite inputs (ValueError)
+        self._ok_in = torch.zeros(1, device=self.device)
         self._acc = torch.zeros(2, device=self.device)
         self.lr_history = [self.optim.lr]
         self._built = True
@@ -248,6 +226,8 @@ class MaPLe(TrainerX):
         self._loss_sum.add_(e.loss_out[0:1])
         self._bad.add_(e.loss_out[3:4])
         self._ok.add_((self._bad == 0).float())
+        self._bad_in.add_(e.input_flag)
+        self._ok_in.add_((self._bad_in == 0).float())
 
     def forward_backward(self, batch):
         """trainers/maple.py:547-627: returns {"loss": float} (one host sync, like loss.item()).  A
@@ -282,8 +262,8 @@ class MaPLe(TrainerX):
         starts the FedAvg exchange there so it overlaps the local test)."""
         self.model.train()
         self._loss_sum.zero_()
-        self._bad.zero_()
-        self._ok.zero_()
+        for t in (self._bad, self._ok, self._bad_in, self._ok_in):
+            t.zero_()
         self.engine.clear_halt()
         steps = 0
         start = self.total_batches
@@ -291,10 +271,14 @@ class MaPLe(TrainerX):
             self.batch_idx = batch_idx
             self._step_async(batch)
             steps += 1
-        bad, ok = self._bad.item(), int(self._ok.item())
+        bad, ok, bad_in, ok_in = torch.cat([self._bad, self._ok, self._bad_in, self._ok_in]).tolist()
+        if bad_in != 0.0 and ok_in <= ok:  # check_tensor_validity (trainers/maple.py:556-557): not caught upstream
+            self.total_batches = start + int(ok_in) + 1
+            self.batch_idx = int(ok_in)
+            raise ValueError("NaN/Inf values in input image")
         if bad != 0.0:  # NaN/Inf loss in this epoch (trainers/maple.py:375-376)
-            self.total_batches = start + ok + 1
-            self.batch_idx = ok
+            self.total_batches = start + int(ok) + 1
+            self.batch_idx = int(ok)
             raise RuntimeError("NaN/Inf in total loss")
         self.update_lr()
         if before_test is not None:

@@ -501,11 +501,34 @@ def test_sgd_and_clip(dev):
     assert abs(out[0].item() - tot_ref) < 1e-3 * tot_ref
     b16 = torch.empty_like(p16)
     b32 = torch.empty_like(p32)
-    hyper = torch.tensor([0.01, 0.9, 5e-4, 1.0], device=dev)
+    # halt set (a non-finite loss earlier in the epoch): nothing changes
+    snap = [t.clone() for t in (p16, g16, p32, g32)]
+    halted = torch.tensor([0.01, 0.9, 5e-4, 1.0, 1.0], device=dev)
+    ops.sgd_step(p16, g16, b16, out, halted)
+    ops.sgd_step(p32, g32, b32, out, halted)
+    assert all(torch.equal(a, b) for a, b in zip(snap, (p16, g16, p32, g32)))
+    hyper = torch.tensor([0.01, 0.9, 5e-4, 1.0, 0.0], device=dev)
     ops.sgd_step(p16, g16, b16, out, hyper)
     ops.sgd_step(p32, g32, b32, out, hyper)
     assert (p16 != rp16.detach()).float().mean().item() < 1e-3
     torch.testing.assert_close(p32, rp32.detach(), rtol=1e-6, atol=1e-7)
+
+
+def test_fedavg_reduce_ordered_kernel(dev):
+    """mf_fedavg_reduce_ordered == the client-order fp32 sum of torch.stack(...) (trainers/maple_fed.py:311-314),
+    bit for bit, for 1..8 clients, ragged lengths and a row stride larger than the length."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    for nclients in (1, 2, 3, 8):
+        for n in (1, 7, 4096 + 3):
+            stride = n + 5
+            host = torch.randn(nclients, stride, generator=g) * torch.exp2(torch.randint(-8, 8, (nclients, stride),
+                                                                                          generator=g).float())
+            out = torch.empty(n, device=dev)
+            ops.fedavg_reduce_ordered(host.to(dev).reshape(-1), nclients, out)
+            ref = host[0, :n].clone()
+            for c in range(1, nclients):
+                ref += host[c, :n]
+            assert torch.equal(out.cpu(), ref), (nclients, n)
 
 
 def test_fedavg_kernels_single_client(dev):

@@ -136,7 +136,9 @@ def test_reference_format_checkpoint_strict_load_and_init_weights(dev, tmp_path)
 def test_nonfinite_loss_stops_the_epoch_at_its_step(dev, tmp_path):
     """trainers/maple.py:375-376 + :617-627: the first non-finite loss raises RuntimeError out of the epoch
     with the weights as they were before that step; total_batches counts up to the failing batch.  Here
-    step 2 of 4 sees a NaN image (inside the graph-replayed epoch, no per-step host sync)."""
+    image 1 of step 2 (of 4) is finite but saturates fp16 (the patch embedding overflows), inside the
+    graph-replayed epoch with no per-step host sync.  A NaN input instead raises ValueError
+    (check_tensor_validity, :526-535, :556-557), also at its step."""
     cfg = small_cfg(tmp_path, clients=1)
     K = 10
     batches = []
@@ -144,7 +146,10 @@ def test_nonfinite_loss_stops_the_epoch_at_its_step(dev, tmp_path):
         b = syn.client_batch(1, 0, s, 4, K)
         batches.append({"img": torch.from_numpy(b.images).to(dev), "label": torch.from_numpy(b.labels).to(dev),
                         "caption": [""] * 4})
-    batches[2]["img"][1, 0, 5, 5] = float("nan")
+    overflow = dict(batches[2], img=batches[2]["img"].clone())
+    overflow["img"][1] = 60000.0
+    nan_in = dict(batches[2], img=batches[2]["img"].clone())
+    nan_in["img"][1, 0, 5, 5] = float("nan")
 
     class DM:
         def __init__(self, base, train):
@@ -152,7 +157,8 @@ def test_nonfinite_loss_stops_the_epoch_at_its_step(dev, tmp_path):
 
     tr = build_trainer(cfg)
     c = tr.clients[0]
-    c.dm = DM(c.dm, batches)
+    base = c.dm
+    c.dm = DM(base, batches[:2] + [overflow] + batches[3:])
     with pytest.raises(RuntimeError, match="NaN/Inf in total loss"):
         c.run_epoch(0)
     assert c.total_batches == 3 and c.batch_idx == 2
@@ -165,9 +171,18 @@ def test_nonfinite_loss_stops_the_epoch_at_its_step(dev, tmp_path):
         assert torch.equal(got[n], v), n
     # the per-batch API raises at the bad batch itself, and the next good batch trains again
     with pytest.raises(RuntimeError, match="NaN/Inf in total loss"):
-        r.forward_backward(batches[2])
+        r.forward_backward(overflow)
     assert torch.equal(r.engine.flat16, c.engine.flat16) and torch.equal(r.engine.flat32, c.engine.flat32)
+    with pytest.raises(ValueError):
+        r.forward_backward(nan_in)
     r.forward_backward(batches[3])
     assert not torch.equal(r.engine.flat16, c.engine.flat16)
     with pytest.raises(AssertionError, match="Label index out of bounds"):
         r.forward_backward(dict(batches[3], label=batches[3]["label"].clone().fill_(K)))
+    # a NaN image inside an epoch: ValueError at its step, no update from it on
+    tr3 = build_trainer(cfg)
+    c3 = tr3.clients[0]
+    c3.dm = DM(base, batches[:1] + [nan_in] + batches[2:])
+    with pytest.raises(ValueError, match="NaN/Inf values in input image"):
+        c3.run_epoch(0)
+    assert c3.total_batches == 2 and c3.batch_idx == 1
