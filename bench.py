@@ -59,6 +59,17 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(J, K, B, budget_s=30.0, seed=0):
     """The oracle (CPU restatement of the reference, oracle/maple_oracle.py; bit-identical to the
     reference on the same host) timed on the host cores: forward + backward + clip + SGD of one
@@ -83,10 +94,60 @@ def cpu_baseline(J, K, B, budget_s=30.0, seed=0):
         log(f"[bench] cpu step {len(ts)}: {ts[-1]:.1f}s")
     sec = float(np.median(ts[1:])) if len(ts) > 1 else ts[0]
     return {"value": Bs / sec, "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"{len(ts)} step(s) of one client at J={J}, B=1 image, K=1 class prompt "
                       f"({sec:.2f} s/step{', median after the first' if len(ts) > 1 else ''}), torch-CPU fp16 "
-                      f"oracle, {torch.get_num_threads()} threads; workload per-image work 87.6 vs "
+                      f"oracle, {torch.get_num_threads()} threads of {cpu_model()}; workload per-image work 87.6 vs "
                       f"{(B * FLOP_PER_IMAGE + K * FLOP_PER_CLASS) / B / 1e9:.1f} GFLOP"}
+
+
+def side_config(name, dev, world, rank, steps=5, warmup=2, seed=0):
+    """Another BASELINE config on the same ranks, reported beside `value` (never as it): the graph-replayed
+    client step (fwd + bwd + clip + SGD) timed over `steps` steps (max over ranks), and the GEMM family
+    split by tower from one probed eager step (HIP events around every launch, towers serialised)."""
+    J, K, B, desc = CONFIGS[name]
+    names = syn.synthetic_classnames(K, seed)
+    e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed), device=dev)
+    e.set_lr(0.0026)
+    cb = syn.client_batch(seed, rank, 0, B, K)
+    e.img_in.copy_(torch.from_numpy(cb.images))
+    e.label_in.copy_(torch.from_numpy(cb.labels))
+    e.train_step()
+    g = e.capture_train_step()
+    for _ in range(warmup):
+        g.replay()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    a = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - a
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    loss = e.loss()
+    probe = ops.KernelProbe("gemm")
+    e.overlap_towers = False
+    ops.set_probe(probe)
+    e.train_step()
+    ops.set_probe(None)
+    fam = {}
+    for tower in ("text", "vision"):
+        p = probe.summary(f"gemm/{tower}")
+        fam[tower] = {"launches": p["launches"], "avg_launch_us": p["avg_us"], "tflops": p["tflops"],
+                      "mfma_frac": p["tflops"] * 1e12 / MFMA_PEAK_F16, "flop_per_launch": p["flops_per_launch"]}
+    step_flop = B * FLOP_PER_IMAGE + K * FLOP_PER_CLASS
+    out = {"workload": f"{name}: {desc}", "value": world * B * steps / el, "unit": "images/s",
+           "ms_per_step": 1e3 * el / steps, "steps": steps, "loss": loss,
+           "model_tflops": world * step_flop * steps / el / 1e12,
+           "model_mfma_frac": step_flop * steps / el / MFMA_PEAK_F16, "gemm_by_tower": fam}
+    del g, e
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -100,6 +161,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-kernel", default="gemm", choices=["gemm", "attention_fwd"])
     ap.add_argument("--no-eot-mode", action="store_true", help="skip the separately reported EOT-truncated run")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 (K=1000 text side) side metric")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -250,6 +312,42 @@ def main():
 
     eval_full, eval_cached = eval_rate(False), eval_rate(True)
 
+    # ---------------- FedAvg overlapped with the client's last local test() (trainers/maple.py:646; the
+    # trainer starts the exchange there, MaPLeFederated.train): exposed = (pack + exchange started, test
+    # pass, wait + unpack) - (test pass alone), max over ranks, median of 3
+    def test_pass(n=4):
+        for i in range(n):
+            load(i)
+            eng.eval_batch(batches[i % 2][1], acc, reuse_text=i > 0)
+
+    def timed(fn):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - a
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    def overlapped():
+        fed.start()
+        test_pass()
+        fed.finish()
+
+    test_pass()
+    exposed = []
+    for _ in range(3):
+        exposed.append(timed(overlapped) - timed(test_pass))
+    fedavg_exposed_ms = 1e3 * float(np.median(exposed))
+    fed_ar = FedAvgBucket(eng, mode="allreduce")
+    fedavg_allreduce_ms = 1e3 * float(np.median([timed(fed_ar.run) for _ in range(5)]))
+    del fed_ar
+
     # ---------------- the data step in front of the path: the train transform
     # (RandomResizedCrop + flip + Normalize -> fp16, Pillow-exact bicubic) on B decoded PatternNet-size
     # 256x256 RGB images resident in HBM; reported beside `value`, never in it
@@ -342,6 +440,10 @@ def main():
                 "frac": ps["tflops"] * 1e12 / MFMA_PEAK_F16, "traffic": None, "kernel": "attention_fwd_kernel",
                 "avg_launch_us": ps["avg_us"], "flop_per_launch": ps["flops_per_launch"]}
 
+    c5 = None
+    if args.config == "c4" and not args.no_c5:
+        c5 = side_config("c5", dev, world, rank)
+
     out = {
         "metric": "images/sec/node (ViT-B/16 MaPLe fwd+bwd)",
         "value": value,
@@ -360,8 +462,13 @@ def main():
                    "parallelism": f"one federated client per GPU x{world}, FedAvg all-reduce per round",
                    "round": f"{args.steps} local steps + 1 FedAvg", "hipgraph": not args.no_graph},
         "fedavg_ms": fedavg_ms,
+        "fedavg_mode": fed.mode,
+        "fedavg_exposed_ms": fedavg_exposed_ms,
+        "fedavg_allreduce_ms": fedavg_allreduce_ms,
+        "fedavg_bucket_mb": 4.0 * (eng.n16 + eng.n32 + 1) / 1e6,
         "fedavg_valid_clients": fed.n_valid(),
         "eot_truncated_mode": eot_mode,
+        "c5_side": c5,
         "eval_images_per_s": {"text_reencoded_per_batch": eval_full, "text_cached_per_pass": eval_cached,
                               "per_gpu": True},
         "input_transform": input_transform,

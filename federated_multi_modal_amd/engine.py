@@ -550,6 +550,10 @@ class MapleEngine:
 
     # ------------------------------------------------------------------ forward
     def _text_forward(self):
+        with ops.probe_tag("text"):
+            self._text_forward_ops()
+
+    def _text_forward_ops(self):
         P = self.P
         t = self.txt
         ops.text_assemble(self.token_prefix, P["prompt_learner.ctx"], self.token_suffix_run,
@@ -561,6 +565,10 @@ class MapleEngine:
                  b_kmajor=True)
 
     def _vision_forward(self):
+        with ops.probe_tag("vision"):
+            self._vision_forward_ops()
+
+    def _vision_forward_ops(self):
         P = self.P
         v = self.vis
         ops.im2col_patch(self.img_in, self.im2col, self.cfg.dims.vision_patch)
@@ -610,6 +618,10 @@ class MapleEngine:
 
     # ------------------------------------------------------------------ backward
     def _text_backward(self):
+        with ops.probe_tag("text"):
+            self._text_backward_ops()
+
+    def _text_backward_ops(self):
         P, G = self.P, self.G
         t = self.txt
         ops.gemm_nt(self.dtxt, P["text_encoder.text_projection"], self.d_txt_final, epilogue=ops.EPI_NONE)
@@ -624,6 +636,10 @@ class MapleEngine:
         t.lnb.finish()  # the text LayerNorms' dgamma/dbeta, on the text stream (overlaps the vision backward)
 
     def _vision_backward(self):
+        with ops.probe_tag("vision"):
+            self._vision_backward_ops()
+
+    def _vision_backward_ops(self):
         P, G = self.P, self.G
         v = self.vis
         ops.gemm_nt(self.dimg, P["image_encoder.proj"], self.d_vis_post, epilogue=ops.EPI_NONE)

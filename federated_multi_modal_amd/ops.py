@@ -54,11 +54,31 @@ class KernelProbe:
 
 
 _PROBE: Optional[KernelProbe] = None
+_TAG = ""  # the tower a probed GEMM belongs to ("vision" / "text"), set by the engine around each tower
 
 
 def set_probe(probe: Optional[KernelProbe]):
     global _PROBE
     _PROBE = probe
+
+
+class probe_tag:
+    """with ops.probe_tag("text"): GEMM probe records are keyed "gemm/text"."""
+
+    def __init__(self, tag: str):
+        self.tag = tag
+
+    def __enter__(self):
+        global _TAG
+        self.prev, _TAG = _TAG, self.tag
+
+    def __exit__(self, *a):
+        global _TAG
+        _TAG = self.prev
+
+
+def _gkey():
+    return f"gemm/{_TAG}" if _TAG else "gemm"
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -85,7 +105,7 @@ def gemm_nt(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NON
     ld_aux = _ld(aux) if aux is not None else 0
     ev = None
     if _PROBE is not None and _PROBE.wants("gemm"):
-        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), "gemm")
+        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), _gkey())
     call("mf_gemm_nt", _p(A), _ld(A), _p(B), _ld(B), _p(C), _ld(C), M, N, K, _p(bias), _p(aux_in), _p(aux_out),
          ld_aux, epilogue, tile, _s())
     if ev is not None:
@@ -107,7 +127,7 @@ def gemm(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NONE, 
     ld_aux = _ld(aux) if aux is not None else 0
     ev = None
     if _PROBE is not None and _PROBE.wants("gemm"):
-        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), "gemm")
+        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), _gkey())
     call("mf_gemm", _p(A), _ld(A), int(a_kmajor), _p(B), _ld(B), int(b_kmajor), _p(C), _ld(C), M, N, K, _p(bias),
          _p(aux_in), _p(aux_out), ld_aux, epilogue, tile, _s())
     if ev is not None:
@@ -133,7 +153,7 @@ def gemm_splitk(A, B, C, ws, splits=0, a_kmajor=False, b_kmajor=False):
     assert ws.dtype == torch.float32 and C.dtype in (torch.float16, torch.float32)
     ev = None
     if _PROBE is not None and _PROBE.wants("gemm"):
-        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), "gemm")
+        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), _gkey())
     call("mf_gemm_splitk", _p(A), _ld(A), int(a_kmajor), _p(B), _ld(B), int(b_kmajor), _p(C), _ld(C), M, N, K,
          _p(ws), ws.numel(), splits, int(C.dtype == torch.float16), _s())
     if ev is not None:
