@@ -1124,7 +1124,9 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
   if (fwd_variant == 4) {
     // the head's 16-query tiles split evenly over its workgroups (no workgroup without a tile)
     const int qs4 = attn_qsplit(N * H, L), tiles = (L + 15) / 16;
-    const dim3 grid4(N * H, qs4), block4(64 * std::min(16, (tiles + qs4 - 1) / qs4));
+    static const int fw = getenv("MAPFED_ATTN_FWD_WAVES") ? atoi(getenv("MAPFED_ATTN_FWD_WAVES")) : 0;  // A/B knob
+    const int nw4 = fw > 0 ? std::min(fw, (tiles + qs4 - 1) / qs4) : std::min(16, (tiles + qs4 - 1) / qs4);
+    const dim3 grid4(N * H, qs4), block4(64 * nw4);
     const int LP16 = tiles * 16;  // keys staged in 16-row tiles (LP16 % 32 == 16: a half last chunk)
 #define CALLF4(P)                                                                                             \
   if (causal)                                                                                                 \

@@ -115,6 +115,40 @@ def reference_param_specs(cfg: EngineConfig) -> List[Tuple[str, Tuple[int, ...],
     return specs
 
 
+def clip_dims_from_state_dict(sd) -> syn.ClipDims:
+    """CLIP geometry from a checkpoint's tensors, as clip/model.py:750-777 (build_model) infers it.  The
+    MaPLe path is the ViT one (VisionTransformer_MaPLe); MultiModalPromptLearner hard-codes the 768-wide
+    vision and 512-wide text prompts (trainers/maple.py:111-124), i.e. ViT-B/16 and ViT-B/32."""
+    shape = lambda k: tuple(np.shape(sd[k]))
+    if "visual.proj" not in sd:
+        raise NotImplementedError("a ResNet CLIP checkpoint: MaPLe's image encoder is the ViT (clip/model.py:478)")
+    vw = shape("visual.conv1.weight")[0]
+    vl = len([k for k in sd if k.startswith("visual.") and k.endswith(".attn.in_proj_weight")])
+    patch = shape("visual.conv1.weight")[-1]
+    grid = round((shape("visual.positional_embedding")[0] - 1) ** 0.5)
+    tw = shape("ln_final.weight")[0]
+    return syn.ClipDims(embed_dim=shape("text_projection")[1], image_resolution=patch * grid, vision_layers=vl,
+                        vision_width=vw, vision_patch=patch, context_length=shape("positional_embedding")[0],
+                        vocab_size=shape("token_embedding.weight")[0] if "token_embedding.weight" in sd
+                        else syn.VOCAB_SIZE, text_width=tw, text_heads=tw // 64,
+                        text_layers=len({k.split(".")[2] for k in sd if k.startswith("transformer.resblocks")}))
+
+
+def check_dims(d: syn.ClipDims):
+    """The geometry the kernels take: head dim 64, sequence lengths <= 256 (attention), GEMM K a multiple of
+    64 (patch embedding 3*patch^2, widths), the prompt learner's 768 / 512 widths."""
+    Lv = d.grid * d.grid + 1 + N_CTX
+    bad = []
+    if d.vision_width != 768 or d.text_width != 512:
+        bad.append("vision / text width 768 / 512 (trainers/maple.py:111-124 hard-codes them)")
+    if Lv > 256 or d.context_length > 256:
+        bad.append(f"sequence lengths <= 256 (vision {Lv}, text {d.context_length})")
+    if (3 * d.vision_patch ** 2) % 64:
+        bad.append(f"3*patch^2 a multiple of 64 (patch {d.vision_patch})")
+    if bad:
+        raise NotImplementedError("CLIP geometry outside the MI355X path: " + "; ".join(bad))
+
+
 def synthetic_state(cfg: EngineConfig) -> Dict[str, np.ndarray]:
     """Synthetic values for every spec, keyed by CustomCLIP parameter name (numpy fp32)."""
     d = cfg.dims
@@ -296,6 +330,7 @@ class MapleEngine:
         d = cfg.dims
         self.B, self.K, self.J = cfg.batch, len(cfg.classnames), cfg.prompt_depth
         assert 1 <= self.J <= 12, "PROMPT_DEPTH must be in [1, 12]"
+        check_dims(d)
         self.specs = reference_param_specs(cfg)
         if shared is None:
             vals = state if state is not None else synthetic_state(cfg)
@@ -410,10 +445,15 @@ class MapleEngine:
     def _build_text_constants(self):
         """token prefix / suffix buffers and the EOT gather index (trainers/maple.py:136-149)."""
         cfg = self.cfg
+        d = cfg.dims
         texts = [f"{cfg.ctx_init} {c.replace('_', ' ')}." for c in cfg.classnames]
-        tok = syn.tokenize(texts)
+        tok = syn.tokenize(texts, d.context_length)
         self.tokenized = torch.from_numpy(tok)
-        emb = syn.token_embedding_rows(cfg.seed, tok.reshape(-1)).reshape(len(texts), 77, 512)
+        if self._token_table is not None:  # the checkpoint's token embedding (trainers/maple.py:140-143)
+            emb = self._token_table.cpu()[torch.from_numpy(tok.reshape(-1))].numpy()
+        else:
+            emb = syn.token_embedding_rows(cfg.seed, tok.reshape(-1), d.text_width)
+        emb = emb.reshape(len(texts), d.context_length, d.text_width)
         dev = self.device
         self.token_prefix = torch.from_numpy(emb[:, :1]).to(dev, F16).contiguous()
         self.token_suffix = torch.from_numpy(emb[:, 1 + cfg.n_ctx:]).to(dev, F16).contiguous()

@@ -27,13 +27,14 @@ Gradients flow through CustomCLIP.forward only (the towers are frozen except Lay
 and the reference trains through CustomCLIP.forward as well, trainers/maple.py:588-590)."""
 from __future__ import annotations
 
+import dataclasses
 from typing import Dict, List, Optional
 
 import torch
 import torch.nn as nn
 
 from . import ops
-from .engine import EngineConfig, MapleEngine, N_CTX, _is_trainable
+from .engine import MapleEngine, N_CTX, _is_trainable
 
 F16, F32 = torch.float16, torch.float32
 
@@ -330,10 +331,7 @@ class CustomCLIP(nn.Module):
         if batch == e.B:
             return e
         if batch not in self._eval:
-            cfg = e.cfg
-            self._eval[batch] = MapleEngine(EngineConfig(batch=batch, classnames=cfg.classnames, prompt_depth=e.J,
-                                                         seed=cfg.seed, n_ctx=cfg.n_ctx, ctx_init=cfg.ctx_init,
-                                                         eot_truncate=cfg.eot_truncate), device=e.device, shared=e)
+            self._eval[batch] = MapleEngine(dataclasses.replace(e.cfg, batch=batch), device=e.device, shared=e)
         return self._eval[batch]
 
     def forward(self, image, label=None, caption=None, return_feature=False):

@@ -20,6 +20,7 @@ ValueError (trainers/maple.py:526-535, not caught); kernel failures -> RuntimeEr
 """
 from __future__ import annotations
 
+import dataclasses
 import os
 import os.path as osp
 from typing import Dict, List, Optional
@@ -156,14 +157,16 @@ class MaPLe(TrainerX):
         cfg = self.cfg
         mcfg = cfg.TRAINER.MAPLE
         classnames = self.classnames
-        state = None
+        state, dims = None, None
         backbone = _backbone_file(cfg)
         if backbone:
-            state = _load_clip_weights(backbone, cfg, classnames, mcfg)
+            state, dims = _load_clip_weights(backbone, cfg, classnames, mcfg)
         ecfg = EngineConfig(batch=cfg.DATALOADER.TRAIN_X.BATCH_SIZE, classnames=list(classnames),
                             prompt_depth=mcfg.PROMPT_DEPTH, seed=max(cfg.SEED, 0), n_ctx=mcfg.N_CTX,
                             ctx_init=mcfg.CTX_INIT, momentum=cfg.OPTIM.MOMENTUM,
                             weight_decay=cfg.OPTIM.WEIGHT_DECAY)
+        if dims is not None:
+            ecfg.dims = dims
         if cfg.OPTIM.NAME != "sgd":
             raise NotImplementedError(f"optimizer {cfg.OPTIM.NAME}: the MaPLe configs use sgd")
         self.engine = MapleEngine(ecfg, device=self.device, state=state)
@@ -299,9 +302,7 @@ class MaPLe(TrainerX):
     # ---------------------------------------------------------------- evaluation
     def _evaluator(self, batch_size: int) -> MapleEngine:
         if self._eval_engine is None or self._eval_engine.B != batch_size:
-            ecfg = EngineConfig(batch=batch_size, classnames=self.engine.cfg.classnames,
-                                prompt_depth=self.engine.J, seed=self.engine.cfg.seed, n_ctx=self.engine.cfg.n_ctx,
-                                ctx_init=self.engine.cfg.ctx_init)
+            ecfg = dataclasses.replace(self.engine.cfg, batch=batch_size)
             self._eval_engine = MapleEngine(ecfg, device=self.device, shared=self.engine)
         return self._eval_engine
 
@@ -396,17 +397,19 @@ def _load_clip_weights(path, cfg, classnames, mcfg):
     """A CLIP checkpoint: a state dict saved with torch.save (loaded with weights_only=True: no code
     runs), or the TorchScript archive clip._download fetches (its parameters are read through
     torch.jit.load, as load_clip_to_cpu does first, trainers/maple.py:27-31)."""
-    import numpy as np
-    from .engine import engine_state_from_clip
+    from .engine import check_dims, clip_dims_from_state_dict, engine_state_from_clip
     try:
         sd = torch.load(path, map_location="cpu", weights_only=True)
     except Exception:  # the official archives are TorchScript (zip with code/), not a plain state dict
         sd = torch.jit.load(path, map_location="cpu").state_dict()
     if isinstance(sd, dict) and "state_dict" in sd:
         sd = sd["state_dict"]
+    sd = {k: v.float().numpy() for k, v in sd.items() if k not in ("input_resolution", "context_length", "vocab_size")}
+    dims = clip_dims_from_state_dict(sd)  # clip/model.py:750-777
+    check_dims(dims)
     ecfg = EngineConfig(batch=1, classnames=list(classnames), prompt_depth=mcfg.PROMPT_DEPTH, seed=max(cfg.SEED, 0),
-                        n_ctx=mcfg.N_CTX, ctx_init=mcfg.CTX_INIT)
-    return engine_state_from_clip({k: v.float().numpy() for k, v in sd.items()}, ecfg)
+                        n_ctx=mcfg.N_CTX, ctx_init=mcfg.CTX_INIT, dims=dims)
+    return engine_state_from_clip(sd, ecfg), dims
 
 
 @TRAINER_REGISTRY.register()

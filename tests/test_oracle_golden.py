@@ -216,3 +216,29 @@ def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
     with pytest.raises(_lib.MapfedError):
         _lib.lib()
     monkeypatch.setattr(_lib, "_LIB", None)
+
+
+def test_clip_dims_inferred_from_state_dict():
+    """clip/model.py:750-777: the geometry comes from the checkpoint's tensor shapes (ViT-B/16 and -B/32
+    load; ResNet and other widths are refused with the reason)."""
+    from federated_multi_modal_amd.engine import check_dims, clip_dims_from_state_dict
+    d = clip_dims_from_state_dict(syn.clip_state_dict(0, vision_layers=2, text_layers=3))
+    assert (d.vision_width, d.vision_patch, d.grid, d.image_resolution, d.vision_layers) == (768, 16, 14, 224, 2)
+    assert (d.text_width, d.text_heads, d.text_layers, d.context_length, d.embed_dim) == (512, 8, 3, 77, 512)
+    check_dims(d)
+    b32 = {"visual.proj": np.empty((768, 512)), "visual.conv1.weight": np.empty((768, 3, 32, 32)),
+           "visual.positional_embedding": np.empty((50, 768)), "text_projection": np.empty((512, 512)),
+           "positional_embedding": np.empty((77, 512)), "token_embedding.weight": np.empty((49408, 512)),
+           "ln_final.weight": np.empty(512)}
+    for i in range(12):
+        b32[f"visual.transformer.resblocks.{i}.attn.in_proj_weight"] = np.empty((2304, 768))
+        b32[f"transformer.resblocks.{i}.attn.in_proj_weight"] = np.empty((1536, 512))
+    d32 = clip_dims_from_state_dict(b32)
+    assert (d32.vision_patch, d32.grid, d32.image_resolution, d32.vision_layers, d32.text_layers) == (32, 7, 224, 12, 12)
+    check_dims(d32)
+    with pytest.raises(NotImplementedError):
+        clip_dims_from_state_dict({"visual.layer1.0.conv1.weight": np.empty((64, 3, 3, 3))})
+    l14 = dict(b32, **{"visual.conv1.weight": np.empty((1024, 3, 14, 14)),
+                       "visual.positional_embedding": np.empty((257, 1024))})
+    with pytest.raises(NotImplementedError):
+        check_dims(clip_dims_from_state_dict(l14))

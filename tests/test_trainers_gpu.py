@@ -186,3 +186,40 @@ def test_nonfinite_loss_stops_the_epoch_at_its_step(dev, tmp_path):
     with pytest.raises(ValueError, match="NaN/Inf values in input image"):
         c3.run_epoch(0)
     assert c3.total_batches == 2 and c3.batch_idx == 1
+
+
+def test_backbone_checkpoint_file(dev, tmp_path):
+    """load_clip_to_cpu + build_model (trainers/maple.py:21-40, clip/model.py:750-793) from a CLIP state-dict
+    file (MODEL.BACKBONE.PATH; the download is offline): geometry inferred from the tensors, every tower
+    parameter equal to the file's tensor in the reference's fp16 / fp32 policy (convert_weights), the
+    prompt prefix / suffix rows and ctx taken from the file's token embedding (trainers/maple.py:96-103,
+    140-143), CLIP's own logit_scale kept as clip_model2.logit_scale, MaPLe's as ln(1/0.07)."""
+    sd = syn.clip_state_dict(7, full_token_table=True)
+    sd["logit_scale"] = np.array(4.6052, dtype=np.float32)  # a trained CLIP's value (ln 100)
+    half = ("conv1.weight", "in_proj_weight", "in_proj_bias", "out_proj.weight", "out_proj.bias", "c_fc.weight",
+            "c_fc.bias", "c_proj.weight", "c_proj.bias", "visual.proj", "text_projection")
+    tsd = {k: torch.from_numpy(np.ascontiguousarray(v)).to(torch.float16 if k.endswith(half) else torch.float32)
+           for k, v in sd.items()}
+    path = tmp_path / "ViT-B-16-state.pt"
+    torch.save(tsd, path)
+    cfg = small_cfg(tmp_path, clients=1, epochs=1, extra=["MODEL.BACKBONE.PATH", str(path)])
+    tr = build_trainer(cfg)
+    e = tr.clients[0].engine
+    for k, v in tsd.items():
+        if k.startswith("visual."):
+            name = "image_encoder." + k[7:]
+        elif k.startswith("transformer.") or k in ("positional_embedding", "ln_final.weight", "ln_final.bias",
+                                                    "text_projection"):
+            name = "text_encoder." + k
+        else:
+            continue
+        assert torch.equal(e.P[name].cpu(), v.to(e.P[name].dtype)), name
+    tok = e.tokenized
+    table = tsd["token_embedding.weight"]
+    assert torch.equal(e.token_prefix.cpu(), table[tok[:, :1]].half())
+    assert torch.equal(e.token_suffix.cpu(), table[tok[:, 3:]].half())
+    init = syn.tokenize(cfg.TRAINER.MAPLE.CTX_INIT)[0, 1:3]
+    assert torch.equal(e.P["prompt_learner.ctx"].cpu(), table[torch.from_numpy(init)].half())
+    assert abs(float(e.clip_logit_scale) - 4.6052) < 1e-6 and abs(float(e.P["logit_scale"]) - np.log(1 / 0.07)) < 1e-6
+    res = tr.clients[0].forward_backward(next(iter(tr.clients[0].dm.train_loader)))
+    assert np.isfinite(res["loss"])
