@@ -79,9 +79,21 @@ __device__ unsigned long long* g_astamps;
   do {                                                                                    \
     if (threadIdx.x == 0 && blockIdx.y == 0) g_astamps[(size_t)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+// every workgroup of a 2-D grid (fwd4): slot 7 = the hardware id (XCC / CU) at the start
+#define MF_ASTAMP2(slot)                                                                  \
+  do {                                                                                    \
+    if (threadIdx.x == 0) {                                                               \
+      const size_t wg_ = (size_t)blockIdx.x * gridDim.y + blockIdx.y;                     \
+      g_astamps[wg_ * 8 + (slot)] = __builtin_amdgcn_s_memrealtime();                     \
+      if ((slot) == 0) g_astamps[wg_ * 8 + 7] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)); \
+    }                                                                                     \
+  } while (0)
 #else
 #define MF_ASTAMP(slot) \
   do {                  \
+  } while (0)
+#define MF_ASTAMP2(slot) \
+  do {                   \
   } while (0)
 #endif
 
@@ -655,6 +667,7 @@ __global__ __launch_bounds__(1024) void attn_fwd4_kernel(const f16* __restrict__
   const int qstep = gridDim.y * nw * 16;
   int q0 = (blockIdx.y * nw + w) * 16;
   const bool active = q0 < L;
+  MF_ASTAMP2(0);
   f16x8 qf0, qf1;
   {
     const int q = q0 + fr;
@@ -679,8 +692,10 @@ __global__ __launch_bounds__(1024) void attn_fwd4_kernel(const f16* __restrict__
   }
   wait_vmcnt(nv);   // Q and this wave's K landed
   __syncthreads();  // ... and every wave's K
+  MF_ASTAMP2(1);
   fwd4_tile<LKP, CAUSAL, true>(sK, sV, koff, voff, qf0, qf1, active, q0, L, lane, out, ld_out, lse, ld_lse,
                                (int64_t)n * L, h, nh);
+  MF_ASTAMP2(2);
   for (q0 += qstep; q0 < L; q0 += qstep) {
     const int q = q0 + fr;
     const f16* qrow = base + (int64_t)(q < L ? q : L - 1) * ld_qkv + h * 64 + 8 * fg;
@@ -689,6 +704,7 @@ __global__ __launch_bounds__(1024) void attn_fwd4_kernel(const f16* __restrict__
     fwd4_tile<LKP, CAUSAL, false>(sK, sV, koff, voff, qf0, qf1, true, q0, L, lane, out, ld_out, lse, ld_lse,
                                   (int64_t)n * L, h, nh);
   }
+  MF_ASTAMP2(3);
 }
 
 // Dq[nh][q] = sum_d dO[q][d] * O[q][d] (fp32) ------------------------------------------------

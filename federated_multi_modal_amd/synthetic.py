@@ -260,6 +260,23 @@ def prompt_learner_params(seed: int, prompt_depth: int, n_ctx: int = 2, text_wid
     return p
 
 
+_CAP_WORDS = ["dense", "sparse", "green", "river", "road", "field", "roof", "forest", "harbor", "runway",
+              "parking", "lot", "bridge", "lake", "farmland", "residential", "industrial", "beach", "desert",
+              "meadow", "highway", "airplane", "cars", "trees", "buildings", "with", "near", "many", "a", "the"]
+
+
+def synthetic_captions(seed: int, client_id: int, step: int, batch: int) -> List[str]:
+    """BLIP-style caption strings for a batch (the reference's datasets carry one per image,
+    datasets/patternnet.py Datum.caption); the first is empty, as a missing caption arrives."""
+    out = []
+    for b in range(batch):
+        u = uniform(seed, f"caption/c{client_id}/s{step}/{b}", 12)
+        n = 0 if b == 0 else 3 + int(u[0] * 8)
+        out.append(" ".join(["a", "satellite", "image", "of"] + [_CAP_WORDS[int(x * len(_CAP_WORDS))] for x in u[1:1 + n]])
+                   if n else "")
+    return out
+
+
 @dataclass
 class ClientBatch:
     images: np.ndarray   # [B,3,224,224] float32 (already "normalized")

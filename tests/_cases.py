@@ -20,7 +20,13 @@ TRACE_SAMPLE = 2048
 
 
 def case_names() -> List[str]:
-    return sorted(p.stem[len("case_"):] for p in GOLD.glob("case_*.npz"))
+    """Caption-free fixtures (eval logits + train loss, optionally gradients and block traces)."""
+    return sorted(p.stem[len("case_"):] for p in GOLD.glob("case_*.npz") if not p.stem.startswith("case_cap_"))
+
+
+def caption_case_names() -> List[str]:
+    """Fixtures of the caption-conditioned path (K19): train loss, gradients, growing vision block traces."""
+    return sorted(p.stem[len("case_"):] for p in GOLD.glob("case_cap_*.npz"))
 
 
 def load_case(name: str) -> Dict[str, np.ndarray]:

@@ -24,12 +24,12 @@ int main(int argc, char** argv) {
   hipMemcpy(qkv, h.data(), (size_t)R * 3 * D * 2, hipMemcpyHostToDevice);
   hipMemcpy(dout, h.data(), (size_t)R * D * 2, hipMemcpyHostToDevice);
   unsigned long long* st;
-  hipMalloc(&st, (size_t)NH * 64);
+  hipMalloc(&st, (size_t)NH * 64 * 8);
   hipMemcpyToSymbol(HIP_SYMBOL(g_astamps), &st, sizeof(st));
   const bool fwd = getenv("STAMP_FWD") != nullptr;  // time the forward (attn_fwd_kernel) instead
   mf_attention_fwd(qkv, 3 * D, o, D, lse, L, N, L, H, causal, 0);
   for (int rep = 0; rep < 5 && fwd; ++rep) {
-    hipMemset(st, 0, (size_t)NH * 64);
+    hipMemset(st, 0, (size_t)NH * 64 * 8);
     mf_attention_fwd(qkv, 3 * D, o, D, lse, L, N, L, H, causal, 0);
     hipDeviceSynchronize();
   }
@@ -38,6 +38,28 @@ int main(int argc, char** argv) {
     int rc = mf_attention_bwd(qkv, 3 * D, o, D, dout, D, lse, ws, L, dqkv, 3 * D, N, L, H, causal, 0);
     if (rc) { printf("error %s\n", mf_last_error()); return 1; }
     hipDeviceSynchronize();
+  }
+  if (fwd && getenv("STAMP_FWD4")) {  // attn_fwd4_kernel: every workgroup, id = x * qsplit + y
+    const int qs = atoi(getenv("STAMP_FWD4"));
+    const int nwg = NH * qs;
+    std::vector<unsigned long long> s((size_t)nwg * 8);
+    hipMemcpy(s.data(), st, s.size() * 8, hipMemcpyDeviceToHost);
+    unsigned long long t0 = ~0ull, t3 = 0;
+    for (int b = 0; b < nwg; ++b) { t0 = std::min(t0, s[b * 8]); t3 = std::max(t3, s[b * 8 + 3]); }
+    printf("fwd4 N=%d L=%d H=%d: %d workgroups, span %.2f us\n", N, L, H, nwg, (t3 - t0) / 100.0);
+    const char* fn[3] = {"stage K", "tile 1", "rest"};
+    for (int k = 0; k < 3; ++k) {
+      std::vector<double> v;
+      for (int b = 0; b < nwg; ++b) v.push_back((s[b * 8 + k + 1] - s[b * 8 + k]) / 100.0);
+      std::sort(v.begin(), v.end());
+      printf("  %-8s min %7.2f  med %7.2f  p90 %7.2f  max %7.2f us\n", fn[k], v[0], v[v.size() / 2], v[v.size() * 9 / 10], v.back());
+    }
+    std::vector<double> st0, en;
+    for (int b = 0; b < nwg; ++b) { st0.push_back((s[b * 8] - t0) / 100.0); en.push_back((s[b * 8 + 3] - t0) / 100.0); }
+    std::sort(st0.begin(), st0.end()); std::sort(en.begin(), en.end());
+    printf("  start    min %7.2f  med %7.2f  p90 %7.2f  max %7.2f us\n", st0[0], st0[st0.size() / 2], st0[st0.size() * 9 / 10], st0.back());
+    printf("  end      min %7.2f  med %7.2f  p90 %7.2f  max %7.2f us\n", en[0], en[en.size() / 2], en[en.size() * 9 / 10], en.back());
+    return 0;
   }
   if (fwd) {  // attn_fwd_kernel: grid (N*H, qsplit); only blockIdx.y == 0 records (its block id = x)
     std::vector<unsigned long long> s((size_t)NH * 8);

@@ -251,6 +251,69 @@ def make_c5_text(seed=0, J=9, K=1000, B=2):
     print(f"case c5_text_k1000: ref {t_ref:.1f}s total {time.time() - t0:.1f}s fp16-vs-fp64 logits {d:.2e}")
 
 
+CAPTION_CASES = [
+    # (name, seed, client, step, J, K, B, caption seed): the caption-conditioned visual prompts (K19)
+    ("cap_c1_j3_b4", 0, 0, 0, 3, 10, 4, 1234),
+    ("cap_j9_k10_b4", 0, 1, 0, 9, 10, 4, 99),
+]
+
+
+def make_caption_case(name, seed, client, step, J, K, B, cap_seed, lr=0.0026):
+    """The reference's training forward + backward with a caption list (trainers/maple.py:307-322 ->
+    clip/model.py:550-561), its global generator seeded with cap_seed right before the call, so the
+    AttentionPooling vector and the Linear(512, 768) it draws are the ones captions.draw_caption_weights
+    draws from a generator seeded the same way.  Stores the loss, every gradient, the image features and
+    every vision block's output (the sequence grows by B rows per prompted layer)."""
+    names = syn.synthetic_classnames(K, seed)
+    batch = syn.client_batch(seed, client, step, B, K)
+    caps = syn.synthetic_captions(seed, client, step, B)
+    img, lab = torch.from_numpy(batch.images), torch.from_numpy(batch.labels)
+    t0 = time.time()
+    ref = h.build_reference_model(seed, J, names)
+    out = {"seed": np.array(seed), "client": np.array(client), "step": np.array(step), "J": np.array(J),
+           "K": np.array(K), "B": np.array(B), "lr": np.array(lr), "labels": batch.labels,
+           "cap_seed": np.array(cap_seed), "captions": np.array(caps)}
+    # the random tensors the forward below draws, drawn the same way beforehand by the reference's own
+    # classes (AttentionPooling, clip/model.py:457-462; nn.Linear(512, 768).half(), :557)
+    model_mod, _, _ = h.load_reference()
+    with h.cuda_as_cpu():
+        torch.manual_seed(cap_seed)
+        ap = model_mod.AttentionPooling(512)
+        lin = torch.nn.Linear(512, 768).half().to("cuda")
+    out["cap_w"] = ap.attention_weights.detach().float().numpy()
+    out["cap_b"] = lin.bias.detach().float().numpy()
+    wl = lin.weight.detach().double().reshape(-1).numpy()
+    out["cap_W_norm"] = np.array(np.linalg.norm(wl))
+    out["cap_W_idx"] = sample_idx("cap_W", wl.size)
+    out["cap_W_val"] = wl[out["cap_W_idx"]].astype(np.float32)
+    trace: dict = {}
+    hooks = _hook_reference(ref, trace)
+    feats = {}
+    hooks.append(ref.image_encoder.register_forward_hook(lambda m, i, o: feats.__setitem__("img", o.detach())))
+    ref.train()
+    with h.cuda_as_cpu():
+        torch.manual_seed(cap_seed)
+        loss = ref(img, lab, caps)
+    for hk in hooks:
+        hk.remove()
+    loss.backward()
+    out["loss"] = np.array(loss.item(), dtype=np.float32)
+    out["img_feat"] = feats["img"].float().numpy()
+    tr = {n: p for n, p in ref.named_parameters() if p.requires_grad}
+    pack_tensors("grad/", {n: p.grad for n, p in tr.items() if p.grad is not None}, out)
+    for key, x in trace.items():
+        if not key.startswith("vision/"):
+            continue
+        flat = x.double().reshape(-1).numpy()
+        idx = trace_idx(name, key, flat.size)
+        out[f"trace/{key}/shape"] = np.array(x.shape)
+        out[f"trace/{key}/norm"] = np.array(np.linalg.norm(flat))
+        out[f"trace/{key}/val"] = flat[idx].astype(np.float32)
+    np.savez_compressed(HERE / f"case_{name}.npz", **out)
+    print(f"caption case {name}: J={J} K={K} B={B} {time.time() - t0:.1f}s loss {out['loss']:.5f} "
+          f"vision lengths {[int(out[f'trace/vision/{i}/shape'][1]) for i in range(12)]}")
+
+
 def make_state_dict_keys():
     """The reference CustomCLIP.state_dict() key set, shapes and dtypes (trainers/maple.py:221-229) at
     J=3 and J=9, and the dtypes FedAvg leaves in the aggregator checkpoint (every key .half(),
@@ -279,3 +342,6 @@ if __name__ == "__main__":
         make_c5_text()
     if "keys" in what:
         make_state_dict_keys()
+    if "captions" in what:
+        for c in CAPTION_CASES:
+            make_caption_case(*c)

@@ -138,6 +138,45 @@ def load_reference():
     return model, maple, maple_fed
 
 
+class cuda_as_cpu:
+    """The reference's caption path hard-codes `.to("cuda")` (clip/model.py:461, 554, 557); on this CPU-only
+    host `with cuda_as_cpu():` maps a "cuda" device argument of Tensor.to / Module.to to "cpu" for the
+    duration of the call (test wiring, like the Dassl stubs; the arithmetic is the reference's)."""
+
+    @staticmethod
+    def _fix(args, kwargs):
+        hit = []
+
+        def f(a):
+            if isinstance(a, str) and a.startswith("cuda"):
+                hit.append(1)
+                return "cpu"
+            if isinstance(a, torch.device) and a.type == "cuda":
+                hit.append(1)
+                return torch.device("cpu")
+            return a
+        return tuple(f(a) for a in args), {k: f(v) for k, v in kwargs.items()}, bool(hit)
+
+    def __enter__(self):
+        self.t_to, self.m_to = torch.Tensor.to, torch.nn.Module.to
+        t_to, m_to, fix = self.t_to, self.m_to, self._fix
+
+        def tensor_to(x, *a, **k):
+            a, k, moved = fix(a, k)
+            if moved:  # a device transfer returns a new plain tensor (a Parameter's .to("cuda") is no Parameter)
+                k["copy"] = True
+            return t_to(x, *a, **k)
+
+        def module_to(m, *a, **k):
+            a, k, _ = fix(a, k)
+            return m_to(m, *a, **k)
+        torch.Tensor.to, torch.nn.Module.to = tensor_to, module_to
+        return self
+
+    def __exit__(self, *exc):
+        torch.Tensor.to, torch.nn.Module.to = self.t_to, self.m_to
+
+
 class _NS:
     def __init__(self, **kw):
         for k, v in kw.items():

@@ -242,3 +242,37 @@ def test_clip_dims_inferred_from_state_dict():
                        "visual.positional_embedding": np.empty((257, 1024))})
     with pytest.raises(NotImplementedError):
         check_dims(clip_dims_from_state_dict(l14))
+
+
+@pytest.mark.parametrize("name", C.caption_case_names())
+def test_oracle_caption_path_matches_reference(name):
+    """K19 (clip/model.py:457-476, 550-561): the random AttentionPooling vector and Linear(512, 768) drawn by
+    captions.draw_caption_weights from a generator seeded like the reference's global one equal the
+    reference's draws bit for bit; the oracle's training forward with those captions and weights then gives
+    the reference's loss, image features and every (growing) vision block output bit for bit, and its
+    gradients within the tolerance of the C1 pin."""
+    from federated_multi_modal_amd.captions import draw_caption_weights
+    c = C.load_case(name)
+    J, K, B, seed, names, batch = C.case_inputs(c)
+    w, W, b = draw_caption_weights(torch.Generator().manual_seed(int(c["cap_seed"])))
+    assert np.array_equal(w.float().numpy(), c["cap_w"]) and np.array_equal(b.float().numpy(), c["cap_b"])
+    assert np.array_equal(W.double().reshape(-1).numpy()[c["cap_W_idx"]].astype(np.float32), c["cap_W_val"])
+    M = O.build_model(seed, J, names)
+    tr: dict = {}
+    caps = [str(x) for x in c["captions"]]
+    loss = O.forward(M, torch.from_numpy(batch.images), torch.from_numpy(batch.labels), train=True, trace=tr,
+                     captions=caps, cap_weights=(w, W, b))
+    assert float(loss) == float(c["loss"])
+    assert np.array_equal(tr["img_feat"].float().numpy(), c["img_feat"])
+    for key in C.trace_keys(c):
+        flat = tr[key].double().reshape(-1).numpy()
+        assert tuple(tr[key].shape) == tuple(c[f"trace/{key}/shape"]), key
+        assert np.array_equal(flat[C.trace_idx(name, key, flat.size)].astype(np.float32), c[f"trace/{key}/val"]), key
+    loss.backward()
+    for n, p in M.trainable().items():
+        if f"grad/norm/{n}" not in c:
+            assert p.grad is None, n
+            continue
+        g = p.grad.double().reshape(-1).numpy()
+        ours, ref = C.sel(c, "grad/", n, g)
+        assert np.abs(ours - ref).max() <= 2e-2 * (np.abs(ref).max() + 1e-12), n
