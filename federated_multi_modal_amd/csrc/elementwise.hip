@@ -5,6 +5,8 @@
 //   * deep-prompt inject and its batch reduction backward (clip/model.py:320-349)
 //   * fp16 transpose (dW operands), fp16 column sums (bias grads)
 //   * small linears of the prompt learner (trainers/maple.py:111-131,194-215)
+//   * the caption path (K19, clip/model.py:457-476, 550-561): attention pooling of the caption token
+//     embeddings, and the growing vision sequence at each prompted layer (+ its backward)
 #include "mf_common.h"
 
 namespace {
@@ -139,6 +141,87 @@ __global__ __launch_bounds__(1024) void inject_bwd_kernel(f16* __restrict__ dx, 
         *o = accumulate ? *o + t[e] : t[e];
       }
     }
+  }
+}
+
+// ---------------------------------------------------------------- caption path (K19)
+// Growing sequence at a prompted vision layer with captions (clip/model.py:320-333 fed by :558-559):
+// dst[n, r] = src[n, r]                      r <  Lp - n_ctx   (all but the previous prompt rows)
+//           = cap[r - (Lp - n_ctx)]           next ncap rows    (the projected captions, shared by all n)
+//           = fp16(prompt[r - (L - n_ctx)])   last n_ctx rows   (the layer's deep prompt, .half())
+// L = Lp + ncap.  8 fp16 per thread.
+__global__ void seq_grow_kernel(const f16* __restrict__ src, f16* __restrict__ dst, const f16* __restrict__ cap,
+                                const float* __restrict__ prompt, int N, int Lp, int L, int n_ctx, int D) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)N * L * (D / 8);
+  if (t >= total) return;
+  const int d = (int)(t % (D / 8)) * 8;
+  const int64_t row = t / (D / 8);
+  const int r = (int)(row % L), n = (int)(row / L);
+  const int keep = Lp - n_ctx;
+  f16x8 v;
+  if (r < keep) {
+    v = *(const f16x8*)(src + ((int64_t)n * Lp + r) * D + d);
+  } else if (r < L - n_ctx) {
+    v = *(const f16x8*)(cap + (int64_t)(r - keep) * D + d);
+  } else {
+    const float* p = prompt + (int64_t)(r - (L - n_ctx)) * D + d;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (f16)p[e];
+  }
+  *(f16x8*)(dst + row * D + d) = v;
+}
+
+// its backward into the previous layer's output: dsrc[n, r] = ddst[n, r] for r < Lp - n_ctx, 0 for the
+// previous prompt rows the layer dropped (the caption rows' and the prompt rows' gradients go elsewhere)
+__global__ void seq_grow_bwd_kernel(const f16* __restrict__ ddst, f16* __restrict__ dsrc, int N, int Lp, int L,
+                                    int n_ctx, int D) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)N * Lp * (D / 8);
+  if (t >= total) return;
+  const int d = (int)(t % (D / 8)) * 8;
+  const int64_t row = t / (D / 8);
+  const int r = (int)(row % Lp), n = (int)(row / Lp);
+  f16x8 v = {};
+  if (r < Lp - n_ctx) v = *(const f16x8*)(ddst + ((int64_t)n * L + r) * D + d);
+  *(f16x8*)(dsrc + row * D + d) = v;
+}
+
+// AttentionPooling over one caption per block (clip/model.py:464-476), from the token ids:
+//   emb[t] = fp16(token_embedding[tok[t]])                      (.type(fp16), trainers/maple.py:316)
+//   s[t]   = fp16(emb[t] . w)                                   (torch.matmul, fp32 accumulate)
+//   p      = fp16(softmax(s))                                   (over the T <= 128 tokens, fp32 math)
+//   pooled = fp16(sum_t fp16(emb[t] * p[t]))                    (fp32 accumulate, tokens in order)
+// one wave per token for the scores, one thread per column for the pooled sum.
+__global__ __launch_bounds__(256) void caption_pool_kernel(const int* __restrict__ tok, int T,
+                                                           const float* __restrict__ table, const f16* __restrict__ w,
+                                                           int D, f16* __restrict__ pooled) {
+  __shared__ float s_score[128];
+  __shared__ float s_p[128];
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int* tb = tok + (int64_t)b * T;
+  for (int t = wv; t < T; t += 4) {
+    const float* e = table + (int64_t)tb[t] * D;
+    float s = 0.f;
+    for (int d = lane; d < D; d += 64) s += (float)(f16)e[d] * (float)w[d];
+    s = wave_sum(s);
+    if (lane == 0) s_score[t] = r16(s);
+  }
+  __syncthreads();
+  if (wv == 0) {
+    float m = -INFINITY;
+    for (int t = lane; t < T; t += 64) m = fmaxf(m, s_score[t]);
+    m = wave_max(m);
+    float z = 0.f;
+    for (int t = lane; t < T; t += 64) z += expf(s_score[t] - m);
+    z = wave_sum(z);
+    for (int t = lane; t < T; t += 64) s_p[t] = r16(expf(s_score[t] - m) / z);
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float acc = 0.f;
+    for (int t = 0; t < T; ++t) acc += r16((float)(f16)table[(int64_t)tb[t] * D + d] * s_p[t]);
+    pooled[(int64_t)b * D + d] = (f16)acc;
   }
 }
 
@@ -447,6 +530,37 @@ extern "C" int mf_prompt_inject_bwd(void* dx, int N, int L, int row0, int nrows,
   inject_bwd_kernel<<<dim3((D + 255) / 256, nrows), 1024, 0, (hipStream_t)stream>>>((f16*)dx, N, L, row0, nrows, D,
                                                                                     out, out_f16, accumulate,
                                                                                     zero_rows);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_seq_grow(const void* src, void* dst, const void* cap, const float* prompt, int N, int Lp, int ncap,
+                           int n_ctx, int D, void* stream) {
+  if (N <= 0) return 0;
+  if (D % 8 || Lp < n_ctx || ncap < 0 || n_ctx < 0) return mf_set_error("mf_seq_grow: bad shape", -1);
+  const int L = Lp + ncap;
+  const int64_t total = (int64_t)N * L * (D / 8);
+  seq_grow_kernel<<<nblk(total), 256, 0, (hipStream_t)stream>>>((const f16*)src, (f16*)dst, (const f16*)cap, prompt,
+                                                               N, Lp, L, n_ctx, D);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_seq_grow_bwd(const void* ddst, void* dsrc, int N, int Lp, int ncap, int n_ctx, int D, void* stream) {
+  if (N <= 0) return 0;
+  if (D % 8 || Lp < n_ctx || ncap < 0) return mf_set_error("mf_seq_grow_bwd: bad shape", -1);
+  const int64_t total = (int64_t)N * Lp * (D / 8);
+  seq_grow_bwd_kernel<<<nblk(total), 256, 0, (hipStream_t)stream>>>((const f16*)ddst, (f16*)dsrc, N, Lp, Lp + ncap,
+                                                                   n_ctx, D);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_caption_pool(const int* tokens, int B, int T, const float* table, const void* w, int D, void* pooled,
+                               void* stream) {
+  if (B <= 0) return 0;
+  if (T <= 0 || T > 128) return mf_set_error("mf_caption_pool: 0 < T <= 128 tokens", -1);
+  caption_pool_kernel<<<B, 256, 0, (hipStream_t)stream>>>(tokens, T, table, (const f16*)w, D, (f16*)pooled);
   MF_CHECK_LAUNCH();
   return 0;
 }

@@ -193,37 +193,63 @@ def engine_state_from_clip(clip_sd: Dict[str, np.ndarray], cfg: EngineConfig,
 
 
 class _Tower:
-    """Buffers + forward/backward schedule of one 12-block transformer tower."""
+    """Buffers + forward/backward schedule of one 12-block transformer tower.
+
+    Ls (optional): the input sequence length of every block.  Without it every block runs L rows per
+    sequence and the deep prompt of a prompted block overwrites rows inject_row0.. of its input in place
+    (fused into ln_1).  With it (the vision tower under the caption path, captions.py) a prompted block's
+    input is built from the previous block's output by mf_seq_grow: all but its last n_ctx rows, the ncap
+    caption rows, the block's deep prompt -- Ls[i] = Ls[i-1] + ncap -- and the backward undoes it
+    (mf_seq_grow_bwd, the prompt's gradient reduced over the sequences)."""
 
     def __init__(self, eng: "MapleEngine", name: str, N: int, L: int, D: int, H: int, layers: int,
-                 causal: bool, inject_row0: int):
+                 causal: bool, inject_row0: int, Ls: Optional[List[int]] = None, ncap: int = 0):
         self.e, self.name, self.N, self.L, self.D, self.H = eng, name, N, L, D, H
         self.layers, self.causal, self.row0 = layers, causal, inject_row0
+        self.Ls = list(Ls) if Ls is not None else [L] * layers
+        assert len(self.Ls) == layers and self.Ls[0] == L
+        self.ncap = ncap
+        self.grow = [i > 0 and self.Ls[i] != self.Ls[i - 1] for i in range(layers)]
+        assert not any(self.grow) or all(self.Ls[i] - self.Ls[i - 1] in (0, ncap) for i in range(1, layers))
+        self.L_out = self.Ls[-1]
         dev = eng.device
-        R = N * L
+        Rs = [N * l for l in self.Ls]
+        self.Rs = Rs
+        R = max(Rs)
         self.R = R
         e = lambda *s, dt=F16: torch.empty(*s, device=dev, dtype=dt)
-        self.X = [e(R, D) for _ in range(layers + 1)]
-        self.QKV = [e(R, 3 * D) for _ in range(layers)]
-        self.O = [e(R, D) for _ in range(layers)]
-        self.X1 = [e(R, D) for _ in range(layers)]
-        self.Fp = [e(R, 4 * D) for _ in range(layers)]
-        self.LSE = [e(N * H * L, dt=F32) for _ in range(layers)]
-        self.mean1 = [e(R, dt=F32) for _ in range(layers)]
-        self.rstd1 = [e(R, dt=F32) for _ in range(layers)]
-        self.mean2 = [e(R, dt=F32) for _ in range(layers)]
-        self.rstd2 = [e(R, dt=F32) for _ in range(layers)]
+        # X[i]: input of block i (X[layers]: the tower's output); Y[i]: block i's output buffer -- X[i+1] itself
+        # unless block i+1 grows the sequence
+        self.X = [e(Rs[0], D)]
+        self.Y = []
+        for i in range(layers):
+            if i + 1 < layers and self.grow[i + 1]:
+                self.Y.append(e(Rs[i], D))
+                self.X.append(e(Rs[i + 1], D))
+            else:
+                self.X.append(e(Rs[i], D))
+                self.Y.append(self.X[i + 1])
+        self.QKV = [e(Rs[i], 3 * D) for i in range(layers)]
+        self.O = [e(Rs[i], D) for i in range(layers)]
+        self.X1 = [e(Rs[i], D) for i in range(layers)]
+        self.Fp = [e(Rs[i], 4 * D) for i in range(layers)]
+        self.LSE = [e(N * H * self.Ls[i], dt=F32) for i in range(layers)]
+        self.mean1 = [e(Rs[i], dt=F32) for i in range(layers)]
+        self.rstd1 = [e(Rs[i], dt=F32) for i in range(layers)]
+        self.mean2 = [e(Rs[i], dt=F32) for i in range(layers)]
+        self.rstd2 = [e(Rs[i], dt=F32) for i in range(layers)]
         self.H1 = e(R, D)
         self.H2 = e(R, D)
         self.G = e(R, 4 * D)
         # backward
         self.dX = e(R, D)
+        self.dX2 = e(R, D) if any(self.grow) else None  # the shrunk gradient of a growing block's input
         self.dX1 = e(R, D)
         self.dO = e(R, D)
         self.dH = e(R, D)
         self.dQKV = e(R, 3 * D)
         self.dF = e(R, 4 * D)
-        self.attn_ws = e(N * H * L, dt=F32)
+        self.attn_ws = e(N * H * max(self.Ls), dt=F32)
         # this tower's LayerNorm dgamma/dbeta partials, reduced in one launch at the end of its backward
         self.lnb = ops.LNGradBatch(dev)
         self.cs_ws = e(ops.colsum_ws_floats(R, 4 * D), dt=F32)
@@ -232,7 +258,8 @@ class _Tower:
         # (only where the automatic split count exceeds 1: few 128x128 output tiles)
         use = os.environ.get("MAPFED_DW_SPLITK", "1") != "0"
         shapes = ((3 * D, D), (D, D), (4 * D, D), (D, 4 * D))
-        ws = {s: ops.gemm_splitk_ws_floats(s[0], s[1], R) for s in shapes}
+        Rl = Rs[-1]
+        ws = {s: ops.gemm_splitk_ws_floats(s[0], s[1], Rl) for s in shapes}
         self.dw_split = {s for s in shapes if use and ws[s] > s[0] * s[1]}
         self.dw_ws = e(max(ws[s] for s in self.dw_split), dt=F32) if self.dw_split else None
 
@@ -247,13 +274,15 @@ class _Tower:
         return self.e.G[f"{self.name}.transformer.resblocks.{i}.{key}"]
 
     # ------------------------------------------------------------------------------------------
-    def forward(self, deep_prompts: List[torch.Tensor]):
-        """X[0] must be filled.  deep_prompts[j] (fp32 [n_ctx, D]) is injected before layer j+1."""
-        N, L, D, H = self.N, self.L, self.D, self.H
+    def forward(self, deep_prompts: List[torch.Tensor], cap: Optional[torch.Tensor] = None):
+        """X[0] must be filled.  deep_prompts[j] (fp32 [n_ctx, D]) is injected before layer j+1; cap [ncap, D]
+        (fp16): the caption rows a growing block appends before its prompt."""
+        N, D, H = self.N, self.D, self.H
         for i in range(self.layers):
+            L, R = self.Ls[i], self.Rs[i]
             x = self.X[i]
-            h1 = self.H1
-            if 1 <= i <= len(deep_prompts):  # deep prompts injected into x and ln_1 in one pass
+            h1 = self.H1[:R]
+            if 1 <= i <= len(deep_prompts) and not self.grow[i]:  # prompt injected into x and ln_1 in one pass
                 ops.layernorm_fwd_inject(x, self.p(i, "ln_1.weight"), self.p(i, "ln_1.bias"), h1, self.mean1[i],
                                          self.rstd1[i], deep_prompts[i - 1], L, self.row0, N_CTX)
             else:
@@ -264,13 +293,16 @@ class _Tower:
             ops.attention_fwd(self.QKV[i], N, L, H, self.causal, out=self.O[i], lse=self.LSE[i])
             ops.gemm_nt(self.O[i], self.p(i, "attn.out_proj.weight"), self.X1[i], bias=self.p(i, "attn.out_proj.bias"),
                         aux_in=x, epilogue=ops.EPI_BIAS_RESID)
-            h2 = self.H2
+            h2 = self.H2[:R]
             ops.layernorm_fwd(self.X1[i], self.p(i, "ln_2.weight"), self.p(i, "ln_2.bias"), h2, self.mean2[i],
                               self.rstd2[i])
-            ops.gemm_nt(h2, self.p(i, "mlp.c_fc.weight"), self.G, bias=self.p(i, "mlp.c_fc.bias"), aux_out=self.Fp[i],
+            g = self.G[:R]
+            ops.gemm_nt(h2, self.p(i, "mlp.c_fc.weight"), g, bias=self.p(i, "mlp.c_fc.bias"), aux_out=self.Fp[i],
                         epilogue=ops.EPI_BIAS_GELU)
-            ops.gemm_nt(self.G, self.p(i, "mlp.c_proj.weight"), self.X[i + 1], bias=self.p(i, "mlp.c_proj.bias"),
+            ops.gemm_nt(g, self.p(i, "mlp.c_proj.weight"), self.Y[i], bias=self.p(i, "mlp.c_proj.bias"),
                         aux_in=self.X1[i], epilogue=ops.EPI_BIAS_RESID)
+            if i + 1 < self.layers and self.grow[i + 1]:
+                ops.seq_grow(self.Y[i], self.X[i + 1], cap, deep_prompts[i], N, L, self.ncap, N_CTX, D)
         # self.H1 / H2 / G now hold the last layer's (block 11) tensors, kept for its dW
 
     def _dw(self, dY: torch.Tensor, Xin: torch.Tensor, dW: torch.Tensor, db: torch.Tensor):
@@ -282,38 +314,50 @@ class _Tower:
         ops.colsum(dY, db, self.cs_ws)
 
     def backward(self, n_prompted: int, prompt_grads: List[torch.Tensor]):
-        """self.dX holds d(loss)/d(X[layers]).  On return self.dX = d(loss)/d(X[0]) (the injected rows
-        of prompted layers reduced into prompt_grads[j] for the prompt injected before layer j+1)."""
-        N, L, D, H = self.N, self.L, self.D, self.H
-        dX = self.dX
+        """self.dX[:Rs[-1]] holds d(loss)/d(X[layers]).  On return self.dX[:Rs[0]] = d(loss)/d(X[0]) (the
+        injected rows of prompted layers reduced into prompt_grads[j] for the prompt injected before layer
+        j+1)."""
+        N, D, H = self.N, self.D, self.H
         last = self.layers - 1
         for i in reversed(range(self.layers)):
+            L, R = self.Ls[i], self.Rs[i]
+            dX = self.dX[:R]
+            dF, dH, dO, dQKV = self.dF[:R], self.dH[:R], self.dO[:R], self.dQKV[:R]
             trainable_w = i == last
             # ---- MLP: X[i+1] = X1 + c_proj(gelu(c_fc(ln_2(X1))))
-            ops.gemm_nt(dX, self.wt(i, "mlp.c_proj.weight"), self.dF, aux_in=self.Fp[i], epilogue=ops.EPI_DGELU)
+            ops.gemm_nt(dX, self.wt(i, "mlp.c_proj.weight"), dF, aux_in=self.Fp[i], epilogue=ops.EPI_DGELU)
             if trainable_w:
-                self._dw(dX, self.G, self.g(i, "mlp.c_proj.weight"), self.g(i, "mlp.c_proj.bias"))
-            ops.gemm_nt(self.dF, self.wt(i, "mlp.c_fc.weight"), self.dH, epilogue=ops.EPI_NONE)
+                self._dw(dX, self.G[:R], self.g(i, "mlp.c_proj.weight"), self.g(i, "mlp.c_proj.bias"))
+            ops.gemm_nt(dF, self.wt(i, "mlp.c_fc.weight"), dH, epilogue=ops.EPI_NONE)
             if trainable_w:
-                self._dw(self.dF, self.H2, self.g(i, "mlp.c_fc.weight"), self.g(i, "mlp.c_fc.bias"))
-            self.lnb.bwd(self.dH, self.X1[i], self.p(i, "ln_2.weight"), self.mean2[i], self.rstd2[i], dX,
-                           self.g(i, "ln_2.weight"), self.g(i, "ln_2.bias"), dres=dX)
+                self._dw(dF, self.H2[:R], self.g(i, "mlp.c_fc.weight"), self.g(i, "mlp.c_fc.bias"))
+            self.lnb.bwd(dH, self.X1[i], self.p(i, "ln_2.weight"), self.mean2[i], self.rstd2[i], dX,
+                         self.g(i, "ln_2.weight"), self.g(i, "ln_2.bias"), dres=dX)
             # ---- attention: X1 = X + out_proj(attn(ln_1(X)))
-            ops.gemm_nt(dX, self.wt(i, "attn.out_proj.weight"), self.dO, epilogue=ops.EPI_NONE)
+            ops.gemm_nt(dX, self.wt(i, "attn.out_proj.weight"), dO, epilogue=ops.EPI_NONE)
             if trainable_w:
                 self._dw(dX, self.O[i], self.g(i, "attn.out_proj.weight"), self.g(i, "attn.out_proj.bias"))
-            ops.attention_bwd(self.QKV[i], self.O[i], self.dO, self.LSE[i], N, L, H, self.causal, dqkv=self.dQKV,
+            ops.attention_bwd(self.QKV[i], self.O[i], dO, self.LSE[i], N, L, H, self.causal, dqkv=dQKV,
                               ws=self.attn_ws)
-            ops.gemm_nt(self.dQKV, self.wt(i, "attn.in_proj_weight"), self.dH, epilogue=ops.EPI_NONE)
+            ops.gemm_nt(dQKV, self.wt(i, "attn.in_proj_weight"), dH, epilogue=ops.EPI_NONE)
             if trainable_w:
-                self._dw(self.dQKV, self.H1, self.g(i, "attn.in_proj_weight"), self.g(i, "attn.in_proj_bias"))
-            if 1 <= i <= n_prompted:  # ln_1 backward + the deep prompt's gradient (its rows of dX) in one pass
-                self.lnb.bwd_inject(self.dH, self.X[i], self.p(i, "ln_1.weight"), self.mean1[i], self.rstd1[i], dX,
+                self._dw(dQKV, self.H1[:R], self.g(i, "attn.in_proj_weight"), self.g(i, "attn.in_proj_bias"))
+            if 1 <= i <= n_prompted and not self.grow[i]:
+                # ln_1 backward + the deep prompt's gradient (its rows of dX) in one pass
+                self.lnb.bwd_inject(dH, self.X[i], self.p(i, "ln_1.weight"), self.mean1[i], self.rstd1[i], dX,
                                     self.g(i, "ln_1.weight"), self.g(i, "ln_1.bias"), dX, prompt_grads[i - 1], L,
                                     self.row0, N_CTX)
             else:
-                self.lnb.bwd(self.dH, self.X[i], self.p(i, "ln_1.weight"), self.mean1[i], self.rstd1[i], dX,
+                self.lnb.bwd(dH, self.X[i], self.p(i, "ln_1.weight"), self.mean1[i], self.rstd1[i], dX,
                              self.g(i, "ln_1.weight"), self.g(i, "ln_1.bias"), dres=dX)
+            if self.grow[i]:
+                # the block's input was [previous output minus its last n_ctx rows | captions | prompt]: the
+                # prompt's gradient is its rows summed over the sequences; the previous output gets the rest
+                ops.prompt_inject_bwd(dX, N, L, L - N_CTX, N_CTX, D, prompt_grads[i - 1], accumulate=False,
+                                      zero_rows=False)
+                Lp = self.Ls[i - 1]
+                ops.seq_grow_bwd(dX, self.dX2[:N * Lp], N, Lp, self.ncap, N_CTX, D)
+                self.dX, self.dX2 = self.dX2, self.dX
 
 
 class MapleEngine:
@@ -357,8 +401,15 @@ class MapleEngine:
         G2 = d.grid * d.grid
         self.Lv = G2 + 1 + cfg.n_ctx
         self.G2 = G2
+        Ls = None
+        if cfg.captions:
+            from .captions import vision_lengths
+            Ls = vision_lengths(G2, cfg.n_ctx, d.vision_layers, self.J - 1, self.B)
+            if max(Ls) > 256:
+                raise NotImplementedError(f"caption path: vision sequence of {max(Ls)} rows (> 256) at B={self.B}, "
+                                          f"J={self.J}")
         self.vis = _Tower(self, "image_encoder", self.B, self.Lv, d.vision_width, d.vision_heads, d.vision_layers,
-                          False, G2 + 1)
+                          False, G2 + 1, Ls=Ls, ncap=self.B if cfg.captions else 0)
         self.txt = _Tower(self, "text_encoder", self.K, self.text_len, d.text_width, d.text_heads, d.text_layers,
                           True, 1)
         self._build_io()
@@ -522,7 +573,15 @@ class MapleEngine:
         self.g_shared_ctx = e(N_CTX, dv)
         self.vis_post = e(B, dv)
         self.post_mean, self.post_rstd = e(B, dt_=F32), e(B, dt_=F32)
-        self.cls_rows = torch.arange(0, B * self.Lv, self.Lv, dtype=torch.int32, device=dev)
+        Lo = self.vis.L_out
+        self.cls_rows = torch.arange(0, B * Lo, Lo, dtype=torch.int32, device=dev)
+        if self.cfg.captions:  # caption path inputs (set_captions) and its projected rows
+            self.cap_tokens = torch.zeros(B, d.context_length, device=dev, dtype=torch.int32)
+            self.cap_w = torch.zeros(dt, device=dev, dtype=F16)
+            self.cap_W = torch.zeros(dv, dt, device=dev, dtype=F16)
+            self.cap_b = torch.zeros(dv, device=dev, dtype=F16)
+            self.cap_pooled = e(B, dt)
+            self.cap_rows = e(B, dv)
         self.img_feat = e(B, E)
         self.txt_final = e(K, dt)
         self.fin_mean, self.fin_rstd = e(K, dt_=F32), e(K, dt_=F32)
@@ -553,6 +612,21 @@ class MapleEngine:
                              db=G[pl + f"compound_prompt_projections.{i}.bias"]))
         self.pl_linears = ops.SmallLinearBatch(dev, ents)
 
+
+    def set_captions(self, tokens, weights):
+        """The caption path's per-batch inputs: tokens [B, T] (clip.tokenize of the batch's captions) and the
+        random (w [512], W [768, 512], b [768]) fp16 the reference draws in that forward
+        (captions.draw_caption_weights).  Copied into static buffers (graph-capturable)."""
+        if not self.cfg.captions:
+            raise RuntimeError("engine built without the caption path (EngineConfig.captions)")
+        tok = torch.as_tensor(tokens)
+        if tuple(tok.shape) != tuple(self.cap_tokens.shape):
+            raise ValueError(f"caption tokens {tuple(tok.shape)}; expected {tuple(self.cap_tokens.shape)}")
+        self.cap_tokens.copy_(tok.to(torch.int32), non_blocking=True)
+        w, W, b = weights
+        self.cap_w.copy_(w, non_blocking=True)
+        self.cap_W.copy_(W, non_blocking=True)
+        self.cap_b.copy_(b, non_blocking=True)
 
     def load_batch(self, images: torch.Tensor, labels: Optional[torch.Tensor] = None):
         """Copy a batch into the static input buffers (H2D when given host tensors)."""
@@ -617,7 +691,12 @@ class MapleEngine:
                             self.shared_ctx, self.Xpre, self.B, self.G2, N_CTX, v.D)
         ops.layernorm_fwd(self.Xpre, P["image_encoder.ln_pre.weight"], P["image_encoder.ln_pre.bias"], v.X[0],
                           self.pre_mean, self.pre_rstd)
-        v.forward(self.vis_deep)
+        cap = None
+        if self.cfg.captions:  # AttentionPooling + Linear(512, 768) of the batch's captions (clip/model.py:550-557)
+            ops.caption_pool(self.cap_tokens, self.token_embedding_table(), self.cap_w, self.cap_pooled)
+            ops.gemm_nt(self.cap_pooled, self.cap_W, self.cap_rows, bias=self.cap_b, epilogue=ops.EPI_BIAS)
+            cap = self.cap_rows
+        v.forward(self.vis_deep, cap)
         ops.layernorm_fwd(v.X[-1], P["image_encoder.ln_post.weight"], P["image_encoder.ln_post.bias"], self.vis_post,
                           self.post_mean, self.post_rstd, row_index=self.cls_rows)
         ops.gemm(self.vis_post, P["image_encoder.proj"], self.img_feat, epilogue=ops.EPI_NONE, b_kmajor=True)
@@ -688,8 +767,8 @@ class MapleEngine:
                           self.post_rstd, v.dX, G["image_encoder.ln_post.weight"], G["image_encoder.ln_post.bias"],
                      row_index=self.cls_rows)
         v.backward(self.J - 1, self.g_vis_deep)
-        v.lnb.bwd(v.dX, self.Xpre, P["image_encoder.ln_pre.weight"], self.pre_mean, self.pre_rstd, self.dXpre,
-                     G["image_encoder.ln_pre.weight"], G["image_encoder.ln_pre.bias"])
+        v.lnb.bwd(v.dX[:v.Rs[0]], self.Xpre, P["image_encoder.ln_pre.weight"], self.pre_mean, self.pre_rstd,
+                  self.dXpre, G["image_encoder.ln_pre.weight"], G["image_encoder.ln_pre.bias"])
         ops.prompt_inject_bwd(self.dXpre, self.B, self.Lv, self.G2 + 1, N_CTX, v.D, self.g_shared_ctx,
                               accumulate=False, zero_rows=False)
         v.lnb.finish()

@@ -337,6 +337,25 @@ def prompt_inject_bwd(dx, N, L, row0, nrows, D, out, accumulate=False, zero_rows
          int(accumulate), int(zero_rows), _s())
 
 
+def seq_grow(src, dst, cap, prompt, N, Lp, ncap, n_ctx, D):
+    """dst [N*(Lp+ncap), D] = per sequence: src rows [0, Lp-n_ctx) | cap [ncap, D] | fp16(prompt [n_ctx, D])."""
+    assert src.shape[0] == N * Lp and dst.shape[0] == N * (Lp + ncap) and prompt.dtype == torch.float32
+    call("mf_seq_grow", _p(src), _p(dst), _p(cap), _p(prompt), N, Lp, ncap, n_ctx, D, _s())
+
+
+def seq_grow_bwd(ddst, dsrc, N, Lp, ncap, n_ctx, D):
+    assert ddst.shape[0] == N * (Lp + ncap) and dsrc.shape[0] == N * Lp
+    call("mf_seq_grow_bwd", _p(ddst), _p(dsrc), N, Lp, ncap, n_ctx, D, _s())
+
+
+def caption_pool(tokens, table, w, pooled):
+    """tokens int32 [B, T] on the device, table fp32 [vocab, D], w fp16 [D] -> pooled fp16 [B, D]."""
+    B, T = tokens.shape
+    assert tokens.dtype == torch.int32 and table.dtype == torch.float32 and w.dtype == torch.float16
+    call("mf_caption_pool", _p(tokens), B, T, _p(table), _p(w), table.shape[1], _p(pooled), _s())
+    return pooled
+
+
 def transpose(inp, out):
     R, C = inp.shape
     call("mf_transpose_f16", _p(inp), _ld(inp), _p(out), _ld(out), R, C, _s())

@@ -113,6 +113,19 @@ int mf_prompt_inject_bwd(void* dx, int N, int L, int row0, int nrows, int D, voi
                          int zero_rows, void* stream);
 
 /* ---- helpers for the backward products ------------------------------------------------------ */
+/* ---- caption-conditioned visual prompts (K19; clip/model.py:457-476, 550-561; trainers/maple.py:307-322) */
+/* The growing vision sequence of a prompted layer: dst [N, Lp+ncap, D] = src rows 0..Lp-n_ctx-1 | cap    */
+/* [ncap, D] (fp16, shared by every sequence) | fp16(prompt [n_ctx, D] fp32); replaces the torch.cat of   */
+/* clip/model.py:324-330 fed with cat(projected captions, deep prompt) (:558-559)                          */
+int mf_seq_grow(const void* src, void* dst, const void* cap, const float* prompt, int N, int Lp, int ncap, int n_ctx,
+                int D, void* stream);
+/* its backward into the previous output: dsrc [N, Lp, D] = ddst rows 0..Lp-n_ctx-1, zeros for the dropped */
+/* previous prompt rows                                                                                     */
+int mf_seq_grow_bwd(const void* ddst, void* dsrc, int N, int Lp, int ncap, int n_ctx, int D, void* stream);
+/* AttentionPooling (clip/model.py:464-476) of B captions from their token ids [B, T] (int32), the fp32     */
+/* token-embedding table and the fp16 weight vector w [D]: pooled [B, D] fp16                                */
+int mf_caption_pool(const int* tokens, int B, int T, const float* table, const void* w, int D, void* pooled,
+                    void* stream);
 int mf_transpose_f16(const void* in, int64_t ld_in, void* out, int64_t ld_out, int R, int C, void* stream);
 int mf_colsum_blocks(int R);
 /* out[c] = sum_r in[r,c]; workspace: mf_colsum_blocks(R) * C floats                               */
