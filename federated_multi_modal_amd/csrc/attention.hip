@@ -1113,6 +1113,22 @@ __global__ __launch_bounds__(64 * (LP / (16 * KT))) void attn_bwd_fused_kernel(
     default: return mf_set_error("attention: bad padded length", -1); \
   }
 
+// Sequences of 257..512 rows (the vision tower under the caption path, 199 + 8*B rows at B = 32, J = 9):
+// non-causal only, on the two-pass forward and the dK/dV + dQ backward with K / V (or Q / dO) of the head
+// in LDS (128 KB at 512 rows, one workgroup per CU).
+#define MF_ATTN_DISPATCH_LONG(LP, CALL)                           \
+  switch (LP) {                                                   \
+    case 288: CALL(288); break;                                   \
+    case 320: CALL(320); break;                                   \
+    case 352: CALL(352); break;                                   \
+    case 384: CALL(384); break;                                   \
+    case 416: CALL(416); break;                                   \
+    case 448: CALL(448); break;                                   \
+    case 480: CALL(480); break;                                   \
+    case 512: CALL(512); break;                                   \
+    default: return mf_set_error("attention: bad padded length", -1); \
+  }
+
 inline int padded_len(int L) { return ((L + 31) / 32) * 32; }
 // one workgroup per (sequence, head): up to 8 waves sharing the staged operands, one 16-row tile each
 inline int attn_threads(int L) {
@@ -1132,10 +1148,19 @@ inline int attn_qsplit(int NH, int L) {
 extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* lse, int ld_lse,
                                 int N, int L, int H, int causal, void* stream) {
   if (N <= 0) return 0;
-  if (L <= 0 || L > 256) return mf_set_error("mf_attention_fwd: 0 < L <= 256 required", -1);
+  if (L <= 0 || L > 512) return mf_set_error("mf_attention_fwd: 0 < L <= 512 required", -1);
+  if (L > 256 && causal) return mf_set_error("mf_attention_fwd: causal masks need L <= 256", -1);
   if (ld_lse < L || (ld_qkv % 8) || (ld_out % 4)) return mf_set_error("mf_attention_fwd: bad strides", -1);
   const int LP = padded_len(L);
   hipStream_t st = (hipStream_t)stream;
+  if (L > 256) {
+    const dim3 grid(N * H, attn_qsplit(N * H, L)), block(attn_threads(L));
+#define CALLFL(P) attn_fwd_kernel<P, false><<<grid, block, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H);
+    MF_ATTN_DISPATCH_LONG(LP, CALLFL)
+#undef CALLFL
+    MF_CHECK_LAUNCH();
+    return 0;
+  }
   static const int fwd_variant = getenv("MAPFED_ATTN_FWD") ? atoi(getenv("MAPFED_ATTN_FWD")) : 4;  // A/B knob
   if (fwd_variant == 4) {
     // the head's 16-query tiles split evenly over its workgroups (no workgroup without a tile)
@@ -1213,10 +1238,27 @@ extern "C" int mf_attention_bwd(const void* qkv, int64_t ld_qkv, const void* out
                                 int64_t ld_dout, const float* lse, float* dq_dot_ws, int ld_lse, void* dqkv,
                                 int64_t ld_dqkv, int N, int L, int H, int causal, void* stream) {
   if (N <= 0) return 0;
-  if (L <= 0 || L > 256) return mf_set_error("mf_attention_bwd: 0 < L <= 256 required", -1);
+  if (L <= 0 || L > 512) return mf_set_error("mf_attention_bwd: 0 < L <= 512 required", -1);
+  if (L > 256 && causal) return mf_set_error("mf_attention_bwd: causal masks need L <= 256", -1);
   if (ld_lse < L || (ld_qkv % 8) || (ld_dout % 8) || (ld_dqkv % 4)) return mf_set_error("mf_attention_bwd: bad strides", -1);
   const int LP = padded_len(L);
   hipStream_t st = (hipStream_t)stream;
+  if (L > 256) {
+    const int64_t tot = (int64_t)N * H * L;
+    attn_bwd_dot_kernel<<<(tot + 255) / 256, 256, 0, st>>>((const f16*)out, ld_out, (const f16*)dout, ld_dout,
+                                                          dq_dot_ws, ld_lse, N, L, H);
+    MF_CHECK_LAUNCH();
+    const dim3 grid(N * H, attn_qsplit(N * H, L)), block(attn_threads(L));
+#define CALLBL(P)                                                                                                  \
+  attn_bwd_dkv_kernel<P, false><<<grid, block, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)dout, ld_dout, lse,     \
+                                                      dq_dot_ws, ld_lse, (f16*)dqkv, ld_dqkv, L, H);               \
+  attn_bwd_dq_kernel<P, false><<<grid, block, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)dout, ld_dout, lse,      \
+                                                     dq_dot_ws, ld_lse, (f16*)dqkv, ld_dqkv, L, H);
+    MF_ATTN_DISPATCH_LONG(LP, CALLBL)
+#undef CALLBL
+    MF_CHECK_LAUNCH();
+    return 0;
+  }
   static const int bwd_variant = getenv("MAPFED_ATTN_BWD") ? atoi(getenv("MAPFED_ATTN_BWD")) : 2;  // A/B knob
   if (bwd_variant == 2 && LP <= 224) {
     static const int kt_w = getenv("MAPFED_ATTN_BWD_KT") ? atoi(getenv("MAPFED_ATTN_BWD_KT")) : 1;  // tuning knob

@@ -42,11 +42,15 @@ def unified_classnames(datasets: Sequence[str], seed: int = 0) -> List[str]:
 class _Split:
     images: torch.Tensor  # [N,3,R,R] fp32, device
     labels: torch.Tensor  # [N] int64, device
+    captions: List[str] = None  # one per image (synthetic BLIP-style strings) or None
 
 
 class _Loader:
     def __init__(self, split: _Split, batch: int, shuffle: bool, drop_last: bool, gen: torch.Generator):
         self.s, self.batch, self.shuffle, self.drop_last, self.gen = split, batch, shuffle, drop_last, gen
+
+    def captions(self, idx):
+        return [self.s.captions[k] for k in idx.tolist()]
 
     def __len__(self):
         n = self.s.labels.numel()
@@ -59,14 +63,17 @@ class _Loader:
         for i in range(len(self)):
             idx = order[i * self.batch:(i + 1) * self.batch]
             yield {"img": self.s.images.index_select(0, idx), "label": self.s.labels.index_select(0, idx),
-                   "caption": [""] * idx.numel(), "index": idx}
+                   "caption": self.captions(idx) if self.s.captions is not None else None, "index": idx}
 
 
 class SyntheticClientDataManager:
     """ClientDataManager stand-in: .train_loader / .test_loader / .num_classes / .lab2cname."""
 
     def __init__(self, client_id: int, classnames: List[str], n_train: int, n_test: int, train_batch: int,
-                 test_batch: int, device, seed: int = 0, image_resolution: int = 224):
+                 test_batch: int, device, seed: int = 0, image_resolution: int = 224, captions: bool = False):
+        """captions: batches carry one synthetic caption string per image (the caption-fork datasets' Datum
+        captions), which turns on the caption-conditioned prompts; off, "caption" is None (BASELINE's
+        synthetic configs carry no captions)."""
         self.client_id = client_id
         self._classnames = list(classnames)
         K = len(classnames)
@@ -79,7 +86,8 @@ class SyntheticClientDataManager:
                                      image_resolution)
                 imgs.append(torch.from_numpy(b.images).to(self.device))
                 labs.append(torch.from_numpy(b.labels).to(self.device))
-            return _Split(torch.cat(imgs), torch.cat(labs))
+            caps = syn.synthetic_captions(seed, client_id, zlib.crc32(tag.encode()), n) if captions else None
+            return _Split(torch.cat(imgs), torch.cat(labs), caps)
 
         self.train = make("train", n_train)
         self.test = make("test", n_test)
@@ -105,9 +113,10 @@ class _DecodedLoader:
     Dassl loader + per-image CPU transform workers (trainers/client_datamanager.py:21-103)."""
 
     def __init__(self, packed, labels: torch.Tensor, batch: int, shuffle: bool, drop_last: bool,
-                 gen: torch.Generator, tfm):
+                 gen: torch.Generator, tfm, captions=None):
         self.p, self.labels, self.batch, self.shuffle, self.drop_last, self.gen, self.tfm = (
             packed, labels, batch, shuffle, drop_last, gen, tfm)
+        self.captions = list(captions) if captions is not None else None
 
     def __len__(self):
         n = self.labels.numel()
@@ -124,7 +133,8 @@ class _DecodedLoader:
             geom = self.tfm.geometry(sub.shapes)
             img = self.tfm(sub, geom)
             idx_d = idx.to(self.labels.device)
-            yield {"img": img, "label": self.labels.index_select(0, idx_d), "caption": [""] * len(sel),
+            caps = [self.captions[k] for k in sel] if self.captions is not None else None
+            yield {"img": img, "label": self.labels.index_select(0, idx_d), "caption": caps,
                    "index": idx_d, "geom": geom}
 
 
@@ -136,7 +146,8 @@ class DecodedClientDataManager:
     batches are fp32 [B,3,224,224] as the reference's loaders yield them."""
 
     def __init__(self, client_id: int, classnames: List[str], train_images, train_labels, test_images,
-                 test_labels, train_batch: int, test_batch: int, device, cfg=None, seed: int = 0):
+                 test_labels, train_batch: int, test_batch: int, device, cfg=None, seed: int = 0,
+                 train_captions=None, test_captions=None):
         from types import SimpleNamespace
 
         from . import transforms as T
@@ -159,8 +170,11 @@ class DecodedClientDataManager:
             raise ValueError("one label per image")
         if ytr.numel() and (int(ytr.min()) < 0 or int(ytr.max()) >= len(classnames)):
             raise ValueError("train labels outside [0, num_classes)")
-        self.train_loader = _DecodedLoader(tr, ytr, train_batch, True, len(tr) >= train_batch, g, self.train_tfm)
-        self.test_loader = _DecodedLoader(te, yte, test_batch, False, False, g, self.test_tfm)
+        # captions (Datum.caption of the reference's caption-fork datasets): batches carry them as a list of
+        # str, which turns the caption-conditioned prompts on (trainers/maple.py:307-322)
+        self.train_loader = _DecodedLoader(tr, ytr, train_batch, True, len(tr) >= train_batch, g, self.train_tfm,
+                                           train_captions)
+        self.test_loader = _DecodedLoader(te, yte, test_batch, False, False, g, self.test_tfm, test_captions)
 
     @property
     def num_classes(self) -> int:

@@ -405,8 +405,8 @@ class MapleEngine:
         if cfg.captions:
             from .captions import vision_lengths
             Ls = vision_lengths(G2, cfg.n_ctx, d.vision_layers, self.J - 1, self.B)
-            if max(Ls) > 256:
-                raise NotImplementedError(f"caption path: vision sequence of {max(Ls)} rows (> 256) at B={self.B}, "
+            if max(Ls) > 512:
+                raise NotImplementedError(f"caption path: vision sequence of {max(Ls)} rows (> 512) at B={self.B}, "
                                           f"J={self.J}")
         self.vis = _Tower(self, "image_encoder", self.B, self.Lv, d.vision_width, d.vision_heads, d.vision_layers,
                           False, G2 + 1, Ls=Ls, ncap=self.B if cfg.captions else 0)

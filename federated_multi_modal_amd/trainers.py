@@ -32,6 +32,7 @@ from . import ops
 from .data import DATASET_CLASSES, SyntheticClientDataManager, unified_classnames
 from .engine import EngineConfig, MapleEngine
 from .federated import FedAvgBucket, reduce_local
+from .captions import caption_tokens, draw_caption_weights, has_captions
 from .modules import CustomCLIP
 from .schedule import HostLR
 
@@ -179,6 +180,10 @@ class MaPLe(TrainerX):
         self.scaler = None
         self.register_model(f"MultiModalPromptLearner_{self.client_id}", self.model, self.optim, self.sched)
         self._graphs = {}
+        self._cap_engine: Optional[MapleEngine] = None
+        # the caption path's random AttentionPooling / Linear draws (captions.py): a per-client generator in
+        # place of the reference's global one
+        self._cap_gen = torch.Generator().manual_seed(max(cfg.SEED, 0) * 1000 + (self.client_id or 0))
         self._loss_sum = torch.zeros(1, device=self.device)
         self._bad = torch.zeros(1, device=self.device)
         self._ok = torch.zeros(1, device=self.device)   # steps of the epoch before its first non-finite loss
@@ -201,8 +206,26 @@ class MaPLe(TrainerX):
     def parse_batch_train(self, batch):
         return batch["img"], batch["label"], batch.get("caption")
 
-    def _load(self, image, label):
-        e = self.engine
+    def _engine_for(self, caption) -> MapleEngine:
+        """The training engine for a batch: captions (a list of str, trainers/maple.py:307-322) take the
+        caption-conditioned engine (vision sequence growing by B rows per prompted layer; parameters,
+        gradients and optimizer state shared with the main engine), with this batch's token ids and a
+        fresh draw of the random pooling / projection weights."""
+        if not has_captions(caption):
+            return self.engine
+        if self._cap_engine is None:
+            self._cap_engine = MapleEngine(dataclasses.replace(self.engine.cfg, captions=True), device=self.device,
+                                           shared=self.engine)
+        ce = self._cap_engine
+        if all(isinstance(c, str) for c in caption):
+            tok = caption_tokens(caption, ce.cfg.dims.context_length)
+        else:
+            tok = torch.stack([torch.as_tensor(c) for c in caption]).cpu()
+        ce.set_captions(tok, draw_caption_weights(self._cap_gen))
+        return ce
+
+    def _load(self, image, label, e=None):
+        e = self.engine if e is None else e
         if image.shape[0] != e.B:
             raise ValueError(f"batch of {image.shape[0]} images; the client engine is built for {e.B}")
         if not label.is_floating_point() and label.device.type == "cpu" and label.numel():
@@ -213,17 +236,19 @@ class MaPLe(TrainerX):
         e.img_in.copy_(image, non_blocking=True)
         e.set_labels(label)  # float labels -> KL branch (trainers/maple.py:356-360)
 
-    def _step_async(self, batch):
-        """One forward_backward without host synchronisation; the loss accumulates on the device."""
-        image, label, _ = self.parse_batch_train(batch)
+    def _step_async(self, batch) -> MapleEngine:
+        """One forward_backward without host synchronisation; the loss accumulates on the device.  Returns
+        the engine that ran (captioned batches run on the caption engine)."""
+        image, label, caption = self.parse_batch_train(batch)
         self.total_batches += 1
-        self._load(image, label)
-        e = self.engine
+        e = self._engine_for(caption)
+        self._load(image, label, e)
         e.set_lr(self.optim.lr)
-        g = self._graphs.get(e.soft_labels)  # one captured step per loss branch
+        key = (e.cfg.captions, e.soft_labels)  # one captured step per (caption path, loss branch)
+        g = self._graphs.get(key)
         if g is None:
             e.train_step()          # first step of a branch eager (the first one creates the momentum buffers)
-            self._graphs[e.soft_labels] = e.capture_train_step()
+            self._graphs[key] = e.capture_train_step()
         else:
             g.replay()
         self._loss_sum.add_(e.loss_out[0:1])
@@ -231,6 +256,7 @@ class MaPLe(TrainerX):
         self._ok.add_((self._bad == 0).float())
         self._bad_in.add_(e.input_flag)
         self._ok_in.add_((self._bad_in == 0).float())
+        return e
 
     def forward_backward(self, batch):
         """trainers/maple.py:547-627: returns {"loss": float} (one host sync, like loss.item()).  A
@@ -244,8 +270,8 @@ class MaPLe(TrainerX):
             if lo_hi[0] < 0 or lo_hi[1] >= self.engine.K:
                 raise AssertionError("Label index out of bounds")
         self.engine.clear_halt()
-        self._step_async(batch)
-        out = self.engine.loss_out.tolist()
+        e = self._step_async(batch)
+        out = e.loss_out.tolist()
         loss = out[0]
         if out[3] != 0.0:
             raise RuntimeError("NaN/Inf in total loss")

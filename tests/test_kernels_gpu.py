@@ -231,7 +231,7 @@ def _attn_ref(q, k, v, causal):
 
 @pytest.mark.parametrize("N,L,H,causal", [(4, 199, 12, False), (10, 77, 8, True), (3, 50, 2, False),
                                           (2, 256, 4, True), (2, 16, 3, True), (3, 40, 2, False),
-                                          (1, 230, 2, True)])
+                                          (1, 230, 2, True), (3, 455, 4, False), (2, 300, 3, False)])
 def test_attention_fwd_bwd(dev, N, L, H, causal):
     torch.manual_seed(L)
     D = H * 64

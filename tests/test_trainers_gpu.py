@@ -102,7 +102,7 @@ def test_soft_label_batches_through_the_trainer(dev, tmp_path):
     sbatch = dict(batch, label=soft)
     losses = [c.forward_backward(sbatch)["loss"], c.forward_backward(batch)["loss"],
               c.forward_backward(sbatch)["loss"], c.forward_backward(batch)["loss"]]
-    assert set(c._graphs) == {False, True}
+    assert set(c._graphs) == {(False, False), (False, True)}
     assert all(l == l and abs(l) < 1e3 for l in losses)
     assert c.engine.soft_labels is False
     with pytest.raises(ValueError):
@@ -223,3 +223,34 @@ def test_backbone_checkpoint_file(dev, tmp_path):
     assert abs(float(e.clip_logit_scale) - 4.6052) < 1e-6 and abs(float(e.P["logit_scale"]) - np.log(1 / 0.07)) < 1e-6
     res = tr.clients[0].forward_backward(next(iter(tr.clients[0].dm.train_loader)))
     assert np.isfinite(res["loss"])
+
+
+def test_captioned_batches_through_the_trainer(dev, tmp_path):
+    """Batches with captions (list of str, trainers/maple.py:307-322) take the caption-conditioned path in
+    the client's forward_backward and run_epoch (its own captured step); batches without captions the plain
+    one; both update the same parameters, and the per-batch loss of a captioned batch equals an engine run
+    with the same captions and the same generator draws."""
+    from federated_multi_modal_amd.captions import caption_tokens, draw_caption_weights
+    from federated_multi_modal_amd.data import SyntheticClientDataManager
+    from federated_multi_modal_amd.engine import EngineConfig, MapleEngine
+    cfg = small_cfg(tmp_path, clients=1)
+    tr = build_trainer(cfg)
+    c = tr.clients[0]
+    names = c.engine.cfg.classnames
+    c.dm = SyntheticClientDataManager(0, names, n_train=8, n_test=4, train_batch=4, test_batch=4, device=dev, seed=1,
+                                      captions=True)
+    batch = next(iter(c.dm.train_loader))
+    assert isinstance(batch["caption"], list) and all(isinstance(x, str) for x in batch["caption"])
+    ref = MapleEngine(EngineConfig(batch=4, classnames=names, prompt_depth=3, seed=1, captions=True), device=dev)
+    ref.set_captions(caption_tokens(batch["caption"]),
+                     draw_caption_weights(torch.Generator().manual_seed(1 * 1000 + 0)))
+    ref.load_batch(batch["img"], batch["label"])
+    ref.forward_backward()
+    loss = c.forward_backward(batch)["loss"]
+    assert loss == ref.loss()
+    c.run_epoch(0)
+    assert (True, False) in c._graphs
+    plain = dict(batch, caption=None)
+    c.forward_backward(plain)
+    assert (False, False) in c._graphs
+    assert c._cap_engine.flat16.data_ptr() == c.engine.flat16.data_ptr()
