@@ -54,6 +54,10 @@ class EngineConfig:
     # bit-identical, the backward differs only in fp32 summation order (zero rows fewer in the weight
     # gradients' reductions).  Off by default: the reference computes all 77.
     eot_truncate: bool = False
+    # The caption-conditioned visual prompts (captions.py, clip/model.py:550-561): the vision tower's
+    # prompted blocks each append the batch's B projected caption rows, so block i runs 199 + i*B rows.
+    # Buffers are sized for it at construction; a batch then needs set_captions().
+    captions: bool = False
 
 
 def _is_trainable(name: str) -> bool:
