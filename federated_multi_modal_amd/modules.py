@@ -34,6 +34,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
+from .captions import caption_tokens, draw_caption_weights, has_captions
 from .engine import MapleEngine, N_CTX, _is_trainable
 
 F16, F32 = torch.float16, torch.float32
@@ -310,7 +311,7 @@ class CustomCLIP(nn.Module):
         c.ln_final = self.text_encoder.ln_final
         self.clip_model2 = c
         self._by_name = {n: cache[id(engine.P[n])] for n in engine.trainable_names}
-        self._eval: Dict[int, MapleEngine] = {}
+        self._eval: Dict[object, MapleEngine] = {}
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         """nn.Module.load_state_dict semantics on the engine (MapleEngine.load_state_dict: strict key check
@@ -334,19 +335,37 @@ class CustomCLIP(nn.Module):
             self._eval[batch] = MapleEngine(dataclasses.replace(e.cfg, batch=batch), device=e.device, shared=e)
         return self._eval[batch]
 
+    def _caption_engine(self, batch: int, caption) -> MapleEngine:
+        """The caption path (trainers/maple.py:307-322 -> clip/model.py:550-561) for a batch: an engine with
+        the growing vision sequence (shared parameters), this batch's caption tokens, and the random
+        AttentionPooling vector / Linear(512, 768) drawn from torch's global CPU generator, as the reference
+        draws them in every such forward (captions.draw_caption_weights reproduces its draws)."""
+        e = self.engine[0]
+        key = ("captions", batch)
+        if key not in self._eval:
+            self._eval[key] = MapleEngine(dataclasses.replace(e.cfg, batch=batch, captions=True), device=e.device,
+                                          shared=e)
+        ce = self._eval[key]
+        if all(isinstance(c, str) for c in caption):
+            tok = caption_tokens(list(caption), ce.cfg.dims.context_length)
+        else:
+            tok = torch.stack([torch.as_tensor(c) for c in caption]).cpu()
+        ce.set_captions(tok, draw_caption_weights(torch.default_generator))
+        return ce
+
     def forward(self, image, label=None, caption=None, return_feature=False):
         """trainers/maple.py:304-381: the loss in train mode (label required), the logits [B, K] in eval
-        mode.  caption: only None or empty is on this path (the caption-conditioned prompts of
-        clip/model.py:550-561 are not built into the module API)."""
-        if caption is not None and len(caption) > 0:
-            raise NotImplementedError("caption-conditioned visual prompts are not available through the module API")
-        e = self._engine_for(image.shape[0])
+        mode.  caption: a list of strings (or token tensors) turns on the caption-conditioned visual prompts
+        (clip/model.py:550-561) exactly as in the reference, random weights included (drawn from torch's
+        global generator)."""
+        if has_captions(caption):
+            e = self._caption_engine(image.shape[0], caption)
+        else:
+            e = self._engine_for(image.shape[0])
         e.img_in.copy_(image)
         if self.training:
             if label is None:
                 raise ValueError("train mode needs labels (trainers/maple.py:349-378)")
-            if e is not self.engine[0]:
-                raise ValueError(f"train batches must have the engine's batch size {self.engine[0].B}")
             if not label.is_floating_point():
                 lo, hi = torch.stack([label.min(), label.max()]).tolist()
                 assert lo >= 0 and hi < e.K, "Label index out of bounds"

@@ -125,3 +125,30 @@ def test_reference_training_step_through_the_module(dev):
                     torch.testing.assert_close(ours, ref, rtol=2e-6, atol=1e-8, msg=n)
             assert 0.0 < coef <= 1.0
     assert torch.isfinite(loss.float())
+
+
+def test_module_caption_forward_like_the_reference(dev):
+    """CustomCLIP.forward(image, label, caption) with torch's global generator seeded as the reference's was
+    when it produced tests/golden/case_cap_c1_j3_b4.npz: the same random AttentionPooling / Linear draws, so
+    the loss matches the reference's (2 fp16 ulps) and the engine's caption path bit for bit; loss.backward()
+    fills p.grad for the trainables."""
+    from federated_multi_modal_amd.captions import caption_tokens, draw_caption_weights
+    c = C.load_case("cap_c1_j3_b4")
+    J, K, B, seed, names, batch = C.case_inputs(c)
+    caps = [str(x) for x in c["captions"]]
+    e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed), device=dev)
+    model = CustomCLIP(e).train()
+    img, lab = torch.from_numpy(batch.images).to(dev), torch.from_numpy(batch.labels).to(dev)
+    torch.manual_seed(int(c["cap_seed"]))
+    loss = model(img, lab, caps)
+    ulp = 2.0 ** (np.floor(np.log2(abs(float(c["loss"])))) - 10)
+    assert abs(loss.item() - float(c["loss"])) <= 2 * ulp
+    loss.backward()
+    assert model.prompt_learner.ctx.grad is not None and torch.isfinite(model.prompt_learner.ctx.grad.float()).all()
+    ref = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed, captions=True), device=dev)
+    ref.set_captions(caption_tokens(caps), draw_caption_weights(torch.Generator().manual_seed(int(c["cap_seed"]))))
+    ref.load_batch(img, lab)
+    ref.forward_backward()
+    assert loss.item() == ref.loss()
+    for n in ref.trainable_names:
+        assert torch.equal(dict(model.named_parameters())[n].grad, ref.G[n]), n
