@@ -467,12 +467,33 @@ class MaPLeFederated(TrainerX):
     def _local_client_ids(self) -> List[int]:
         return [self.rank] if self.distributed else list(range(self.num_clients))
 
+    def _disk_datasets(self) -> bool:
+        root = self.cfg.DATASET.ROOT
+        return bool(root) and all(osp.isdir(osp.join(osp.expanduser(root), d)) for d in ("PatternNet", "Ucmerced",
+                                                                                          "eurosat"))
+
     def build_data_loader(self):
         """trainers/maple_fed.py:48-159: the unified class list over the client datasets, then one data
-        manager per client (synthetic splits, see data.py)."""
-        if self.cfg.DATASET.ROOT and osp.isdir(self.cfg.DATASET.ROOT):
-            print(f"[INFO] DATASET.ROOT={self.cfg.DATASET.ROOT}: disk datasets are not wired on this path; "
-                  "using seeded synthetic client splits")
+        manager per client.  With PatternNet / Ucmerced / eurosat under DATASET.ROOT: the disk datasets
+        (datasets.py; client 0 = PatternNet, client 1 = UcMerced, as the reference hard-codes), images decoded
+        on the host and transformed on the device; otherwise seeded synthetic splits of the same shapes
+        (data.py)."""
+        if self._disk_datasets():
+            from . import datasets as dsets
+            if self.num_clients != 2:
+                raise ValueError("the disk datasets give the reference's two clients (PatternNet, UcMerced); "
+                                 f"FED.NUM_CLIENTS is {self.num_clients}")
+            seed = max(self.cfg.SEED, 0)
+            loaded = {n: dsets.load_dataset(n, self.cfg.DATASET.ROOT, self.cfg.DATASET.NUM_SHOTS, seed)
+                      for n in self.CLIENT_DATASETS}
+            names, loaded = dsets.union_and_remap(loaded)
+            print(f"[INFO] Unified #classes = {len(names)}")
+            self.lab2cname = {i: c for i, c in enumerate(names)}
+            self.client_data_managers = {
+                i: dsets.client_data_manager(i, names, loaded[("PatternNet", "Ucmerced")[i]], self.cfg, self.device,
+                                             seed) for i in self._local_client_ids()}
+            self.train_loader_x = self.val_loader = self.test_loader = self.dm = None
+            return
         K = self.cfg.MODEL.NUM_CLASSES
         names = unified_classnames(self.CLIENT_DATASETS, max(self.cfg.SEED, 0))
         if K:

@@ -254,3 +254,28 @@ def test_captioned_batches_through_the_trainer(dev, tmp_path):
     c.forward_backward(plain)
     assert (False, False) in c._graphs
     assert c._cap_engine.flat16.data_ptr() == c.engine.flat16.data_ptr()
+
+
+def test_disk_datasets_round(dev, tmp_path):
+    """DATASET.ROOT with PatternNet / Ucmerced / eurosat trees (tests/test_datasets.py writes the same
+    layout): the aggregator builds the class union (trainers/maple_fed.py:48-159), client 0 trains on
+    PatternNet and client 1 on UcMerced images decoded on the host and transformed on the device, their
+    captions turn on the caption-conditioned path, and a round completes."""
+    import test_datasets as TD
+    root = str(tmp_path / "data")
+    TD._write_tree(root, "PatternNet/images", ["forest", "parking_lot"], 10, "PatternNet/Captions", size=(64, 80))
+    TD._write_tree(root, "Ucmerced/Images", ["forest", "parkinglot", "beach"], 10, "Ucmerced/Captions", size=(72, 64))
+    TD._write_tree(root, "eurosat/2750", ["AnnualCrop"], 10, "eurosat/captions", size=(64, 64))
+    for k in range(10):
+        with open(os.path.join(root, "eurosat/captions/AnnualCrop", f"img_{k:03d}.txt"), "w") as f:
+            f.write("field")
+    cfg = small_cfg(tmp_path, epochs=1, extra=["DATASET.ROOT", root, "DATASET.NUM_SHOTS", 2,
+                                                "DATALOADER.TRAIN_X.BATCH_SIZE", 2, "DATALOADER.TEST.BATCH_SIZE", 4,
+                                                "MODEL.NUM_CLASSES", 0])
+    tr = build_trainer(cfg)
+    assert [c for _, c in sorted(tr.lab2cname.items())] == ["Annual Crop Land", "beach", "forest", "parking_lot"]
+    b = next(iter(tr.clients[1].dm.train_loader))
+    assert b["img"].shape == (2, 3, 224, 224) and isinstance(b["caption"], list)
+    tr.train()
+    assert tr.nan_stats["total_updates"] == 1
+    assert tr.clients[0]._cap_engine is not None  # captioned batches took the caption path
