@@ -220,314 +220,6 @@ __global__ __launch_bounds__(512, 4) void attn_fwd_kernel(const f16* __restrict_
   }
 }
 
-// Forward, one workgroup per (sequence, head): K and V of the head are staged into LDS ONCE and
-// every wave owns QT 16-query tiles (32 queries at QT = 2), so each K / V^T fragment read from LDS
-// feeds QT MFMAs.  Same two-pass numerics as attn_fwd_kernel (P relative to the final row max).
-template <int LKP, bool CAUSAL, int QT>
-__global__ __launch_bounds__(64 * ((LKP + 16 * QT - 1) / (16 * QT)), 2) void attn_fwd2_kernel(
-    const f16* __restrict__ qkv, int64_t ld_qkv, f16* __restrict__ out, int64_t ld_out, float* __restrict__ lse,
-    int ld_lse, int L, int H) {
-  constexpr int NKT = LKP / 16;
-  __shared__ __attribute__((aligned(16))) f16 sK[LKP * 64];
-  __shared__ __attribute__((aligned(16))) f16 sV[LKP * 64];
-  const int D = H * 64;
-  const int nh = blockIdx.x, n = nh / H, h = nh % H;
-  const f16* base = qkv + (int64_t)n * L * ld_qkv;
-  stage_rows<LKP>(sK, base, ld_qkv, L, D + h * 64);
-  stage_rows<LKP>(sV, base, ld_qkv, L, 2 * D + h * 64);
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int fr = lane & 15, fg = lane >> 4, ii = lane & 15;
-  const int q0 = w * 16 * QT;
-  // Q fragments straight to registers (overlapping the K / V DMA)
-  f16x8 qf[QT][2];
-  int qrow[QT];
-#pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    qrow[t] = q0 + 16 * t + fr;
-    const int qc = qrow[t] < L ? qrow[t] : L - 1;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) qf[t][s] = *(const f16x8*)(base + (int64_t)qc * ld_qkv + h * 64 + 32 * s + 8 * fg);
-  }
-  int koff[2][2], voff[4][2];
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const int row = 16 * hf + fr;
-      koff[s2][hf] = row * 64 + (((4 * s2 + fg) ^ (row & 7)) << 3);
-    }
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) voff[dt][hf] = sw_off(16 * hf + 4 * fg + (ii >> 2), 16 * dt + 4 * (ii & 3));
-  }
-  stage_wait();
-  const int kt_end = CAUSAL ? min(NKT, (q0 + 16 * QT + 15) / 16) : NKT;
-  const int ks_end = (kt_end + 1) / 2;
-  auto scores = [&](int ks, f32x4 (&a)[QT][2]) {
-    const f16* kb = sK + ks * 32 * 64;
-#pragma unroll
-    for (int t = 0; t < QT; ++t) a[t][0] = a[t][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const f16x8 k0 = *(const f16x8*)(kb + koff[s2][0]);
-      const f16x8 k1 = *(const f16x8*)(kb + koff[s2][1]);
-#pragma unroll
-      for (int t = 0; t < QT; ++t) {
-        a[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k0, qf[t][s2], a[t][0], 0, 0, 0);
-        a[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k1, qf[t][s2], a[t][1], 0, 0, 0);
-      }
-    }
-    if (CAUSAL || 32 * ks + 32 > L) {
-#pragma unroll
-      for (int t = 0; t < QT; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key0 = 32 * ks + 4 * fg + i, key1 = key0 + 16;
-          if (key0 >= L || (CAUSAL && key0 > qrow[t])) a[t][0][i] = -INFINITY;
-          if (key1 >= L || (CAUSAL && key1 > qrow[t])) a[t][1][i] = -INFINITY;
-        }
-    }
-  };
-  float m[QT];
-#pragma unroll
-  for (int t = 0; t < QT; ++t) m[t] = -INFINITY;
-#pragma unroll 1
-  for (int ks = 0; ks < ks_end; ++ks) {
-    f32x4 a[QT][2];
-    scores(ks, a);
-#pragma unroll
-    for (int t = 0; t < QT; ++t) {
-      m[t] = fmaxf(m[t], fmaxf(fmaxf(a[t][0][0], a[t][0][1]), fmaxf(a[t][0][2], a[t][0][3])));
-      m[t] = fmaxf(m[t], fmaxf(fmaxf(a[t][1][0], a[t][1][1]), fmaxf(a[t][1][2], a[t][1][3])));
-    }
-  }
-  constexpr float kLog2eScale = 0.125f * 1.4426950408889634f;
-  float mb[QT], l[QT];
-  f32x4 oacc[QT][4];
-#pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    m[t] = fmaxf(m[t], __shfl_xor(m[t], 16, 64));
-    m[t] = fmaxf(m[t], __shfl_xor(m[t], 32, 64));
-    mb[t] = -m[t] * kLog2eScale;
-    l[t] = 0.f;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) oacc[t][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll 1
-  for (int ks = 0; ks < ks_end; ++ks) {
-    f32x4 a[QT][2];
-    scores(ks, a);
-    f16x8 pf[QT];
-#pragma unroll
-    for (int t = 0; t < QT; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(a[t][0][i], kLog2eScale, mb[t]));
-        const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(a[t][1][i], kLog2eScale, mb[t]));
-        l[t] += p0 + p1;
-        pf[t][i] = (f16)p0;
-        pf[t][4 + i] = (f16)p1;
-      }
-    const f16* vb = sV + ks * 32 * 64;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[dt][0]));
-      s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[dt][1]));
-      const f16x8 vf = cat8(__builtin_bit_cast(f16x4, v0), __builtin_bit_cast(f16x4, v1));
-#pragma unroll
-      for (int t = 0; t < QT; ++t) oacc[t][dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[t], oacc[t][dt], 0, 0, 0);
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    float lt = l[t];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
-    const int q = qrow[t];
-    if (q < L) {
-      const float inv = 1.0f / lt;
-      f16* orow = out + ((int64_t)n * L + q) * ld_out + h * 64;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        f16x4 o;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = (f16)(oacc[t][dt][i] * inv);
-        *(f16x4*)(orow + 16 * dt + 4 * fg) = o;
-      }
-      if (fg == 0) lse[(int64_t)nh * ld_lse + q] = m[t] * kScale + __logf(lt);
-    }
-  }
-}
-
-// Forward, software-pipelined: the workgroup (NW waves, QT 16-query tiles per wave) covers
-// 16*QT*NW queries of one (sequence, head) (blockIdx.y picks the query block), with K and V of the
-// head staged in LDS.  Same two-pass numerics as attn_fwd_kernel (P relative to the final row max),
-// but in both passes the score MFMAs of key chunk ks+1 are issued before the VALU work of chunk ks
-// (row max / exp / row sum / P pack), so the matrix and vector pipes of a wave overlap instead of
-// alternating, and each K / V^T fragment read from LDS feeds QT MFMAs.
-template <int LKP, bool CAUSAL, int QT, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void attn_fwd3_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
-                                                               f16* __restrict__ out, int64_t ld_out,
-                                                               float* __restrict__ lse, int ld_lse, int L, int H) {
-  constexpr int NKT = LKP / 16;
-  __shared__ __attribute__((aligned(16))) f16 sK[LKP * 64];
-  __shared__ __attribute__((aligned(16))) f16 sV[LKP * 64];
-  const int D = H * 64;
-  const int nh = blockIdx.x, n = nh / H, h = nh % H;
-  const f16* base = qkv + (int64_t)n * L * ld_qkv;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int q0 = (blockIdx.y * NW + w) * 16 * QT;
-  // the workgroup's last query bounds the keys it needs under the causal mask
-  const int kneed = CAUSAL ? min(L, (blockIdx.y + 1) * NW * 16 * QT) : L;
-  stage_rows<LKP>(sK, base, ld_qkv, kneed, D + h * 64);
-  stage_rows<LKP>(sV, base, ld_qkv, kneed, 2 * D + h * 64);
-
-  const int fr = lane & 15, fg = lane >> 4, ii = lane & 15;
-  f16x8 qf[QT][2];
-  int qrow[QT];
-#pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    qrow[t] = q0 + 16 * t + fr;
-    const int qc = qrow[t] < L ? qrow[t] : L - 1;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) qf[t][s2] = *(const f16x8*)(base + (int64_t)qc * ld_qkv + h * 64 + 32 * s2 + 8 * fg);
-  }
-  int koff[2][2], voff[4][2];
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const int row = 16 * hf + fr;
-      koff[s2][hf] = row * 64 + (((4 * s2 + fg) ^ (row & 7)) << 3);
-    }
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) voff[dt][hf] = sw_off(16 * hf + 4 * fg + (ii >> 2), 16 * dt + 4 * (ii & 3));
-  }
-  stage_wait();
-  if (q0 >= L) return;  // a wave past the sequence (after the workgroup's last barrier)
-  const int kt_end = CAUSAL ? min(NKT, (q0 + 16 * QT + 15) / 16) : NKT;
-  const int ks_end = (kt_end + 1) / 2;
-  auto scores = [&](int ks, f32x4 (&a)[QT][2]) {
-    const f16* kb = sK + ks * 32 * 64;
-#pragma unroll
-    for (int t = 0; t < QT; ++t) a[t][0] = a[t][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const f16x8 k0 = *(const f16x8*)(kb + koff[s2][0]);
-      const f16x8 k1 = *(const f16x8*)(kb + koff[s2][1]);
-#pragma unroll
-      for (int t = 0; t < QT; ++t) {
-        a[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k0, qf[t][s2], a[t][0], 0, 0, 0);
-        a[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k1, qf[t][s2], a[t][1], 0, 0, 0);
-      }
-    }
-  };
-  auto mask = [&](int ks, f32x4 (&a)[QT][2]) {
-    if (CAUSAL || 32 * ks + 32 > L) {
-#pragma unroll
-      for (int t = 0; t < QT; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key0 = 32 * ks + 4 * fg + i, key1 = key0 + 16;
-          if (key0 >= L || (CAUSAL && key0 > qrow[t])) a[t][0][i] = -INFINITY;
-          if (key1 >= L || (CAUSAL && key1 > qrow[t])) a[t][1][i] = -INFINITY;
-        }
-    }
-  };
-  // pass 1: row max
-  float m[QT];
-#pragma unroll
-  for (int t = 0; t < QT; ++t) m[t] = -INFINITY;
-  {
-    f32x4 cur[QT][2], nxt[QT][2];
-    scores(0, cur);
-#pragma unroll 1
-    for (int ks = 0; ks < ks_end; ++ks) {
-      if (ks + 1 < ks_end) scores(ks + 1, nxt);
-      mask(ks, cur);
-#pragma unroll
-      for (int t = 0; t < QT; ++t) {
-        m[t] = fmaxf(m[t], fmaxf(fmaxf(cur[t][0][0], cur[t][0][1]), fmaxf(cur[t][0][2], cur[t][0][3])));
-        m[t] = fmaxf(m[t], fmaxf(fmaxf(cur[t][1][0], cur[t][1][1]), fmaxf(cur[t][1][2], cur[t][1][3])));
-      }
-#pragma unroll
-      for (int t = 0; t < QT; ++t) cur[t][0] = nxt[t][0], cur[t][1] = nxt[t][1];
-    }
-  }
-  constexpr float kLog2eScale = 0.125f * 1.4426950408889634f;
-  float mb[QT], l[QT];
-  f32x4 oacc[QT][4];
-#pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    m[t] = fmaxf(m[t], __shfl_xor(m[t], 16, 64));
-    m[t] = fmaxf(m[t], __shfl_xor(m[t], 32, 64));
-    mb[t] = -m[t] * kLog2eScale;
-    l[t] = 0.f;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) oacc[t][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  }
-  // pass 2: P = exp(S - max), row sum, O += V^T P
-  {
-    f32x4 cur[QT][2], nxt[QT][2];
-    scores(0, cur);
-#pragma unroll 1
-    for (int ks = 0; ks < ks_end; ++ks) {
-      if (ks + 1 < ks_end) scores(ks + 1, nxt);
-      const f16* vb = sV + ks * 32 * 64;
-      f16x8 vf[4];
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[dt][0]));
-        s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[dt][1]));
-        vf[dt] = cat8(__builtin_bit_cast(f16x4, v0), __builtin_bit_cast(f16x4, v1));
-      }
-      mask(ks, cur);
-      f16x8 pf[QT];
-#pragma unroll
-      for (int t = 0; t < QT; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(cur[t][0][i], kLog2eScale, mb[t]));
-          const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(cur[t][1][i], kLog2eScale, mb[t]));
-          l[t] += p0 + p1;
-          pf[t][i] = (f16)p0;
-          pf[t][4 + i] = (f16)p1;
-        }
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int t = 0; t < QT; ++t) oacc[t][dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf[dt], pf[t], oacc[t][dt], 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < QT; ++t) cur[t][0] = nxt[t][0], cur[t][1] = nxt[t][1];
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    float lt = l[t];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
-    const int q = qrow[t];
-    if (q < L) {
-      const float inv = 1.0f / lt;
-      f16* orow = out + ((int64_t)n * L + q) * ld_out + h * 64;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        f16x4 o;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = (f16)(oacc[t][dt][i] * inv);
-        *(f16x4*)(orow + 16 * dt + 4 * fg) = o;
-      }
-      if (fg == 0) lse[(int64_t)nh * ld_lse + q] = m[t] * kScale + __logf(lt);
-    }
-  }
-}
-
-// Forward, single pass with register-resident scores: the grid / wave layout of attn_fwd_kernel
-// (16 queries per wave), but every score of the wave's queries (LKP keys x 16 queries = LKP/4 fp32 per
-// lane) is computed ONCE by independent back-to-back MFMAs and kept in registers; row max, exp, row
-// sum and the fp16 P pack then run from registers, and P . V follows.  Bit-identical to
-// attn_fwd_kernel (the same products in the same order; max is exact; the row sum and the P.V
-// accumulation keep its order) with a third fewer MFMAs and K reads and no per-chunk latency chain.
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a constant)
 MF_DEV void wait_vmcnt(int n) {
   switch (n) {
@@ -1161,7 +853,7 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
     MF_CHECK_LAUNCH();
     return 0;
   }
-  static const int fwd_variant = getenv("MAPFED_ATTN_FWD") ? atoi(getenv("MAPFED_ATTN_FWD")) : 4;  // A/B knob
+  static const int fwd_variant = getenv("MAPFED_ATTN_FWD") ? atoi(getenv("MAPFED_ATTN_FWD")) : 4;  // A/B knob: 1 = attn_fwd_kernel
   if (fwd_variant == 4) {
     // the head's 16-query tiles split evenly over its workgroups (no workgroup without a tile)
     const int qs4 = attn_qsplit(N * H, L), tiles = (L + 15) / 16;
@@ -1186,39 +878,6 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
       default: MF_ATTN_DISPATCH(LP, CALLF4)
     }
 #undef CALLF4
-    MF_CHECK_LAUNCH();
-    return 0;
-  }
-  static const int fwd_nw = getenv("MAPFED_ATTN_FWD_NW") ? atoi(getenv("MAPFED_ATTN_FWD_NW")) : 4;   // waves / WG
-  if (fwd_variant == 3) {
-    const int nw = fwd_nw == 8 ? 8 : 4;
-    const dim3 grid3(N * H, (L + 32 * nw - 1) / (32 * nw)), block3(64 * nw);
-#define CALLF3(P)                                                                                                   \
-  if (nw == 8) {                                                                                                    \
-    if (causal)                                                                                                     \
-      attn_fwd3_kernel<P, true, 2, 8><<<grid3, block3, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); \
-    else                                                                                                            \
-      attn_fwd3_kernel<P, false, 2, 8><<<grid3, block3, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); \
-  } else {                                                                                                          \
-    if (causal)                                                                                                     \
-      attn_fwd3_kernel<P, true, 2, 4><<<grid3, block3, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); \
-    else                                                                                                            \
-      attn_fwd3_kernel<P, false, 2, 4><<<grid3, block3, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); \
-  }
-    MF_ATTN_DISPATCH(LP, CALLF3)
-#undef CALLF3
-    MF_CHECK_LAUNCH();
-    return 0;
-  }
-  if (fwd_variant == 2) {
-    const dim3 grid2(N * H), block2(64 * ((L + 31) / 32));
-#define CALLF2(P)                                                                                               \
-  if (causal)                                                                                                   \
-    attn_fwd2_kernel<P, true, 2><<<grid2, block2, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); \
-  else                                                                                                          \
-    attn_fwd2_kernel<P, false, 2><<<grid2, block2, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H);
-    MF_ATTN_DISPATCH(LP, CALLF2)
-#undef CALLF2
     MF_CHECK_LAUNCH();
     return 0;
   }

@@ -24,12 +24,13 @@ int main(int argc, char** argv) {
   hipMemcpy(qkv, h.data(), (size_t)R * 3 * D * 2, hipMemcpyHostToDevice);
   hipMemcpy(dout, h.data(), (size_t)R * D * 2, hipMemcpyHostToDevice);
   unsigned long long* st;
-  hipMalloc(&st, (size_t)NH * 64 * 8);
+  const size_t nst = std::max<size_t>((size_t)NH * 64, 256 * 16 * 8);
+  hipMalloc(&st, nst * 8);
   hipMemcpyToSymbol(HIP_SYMBOL(g_astamps), &st, sizeof(st));
   const bool fwd = getenv("STAMP_FWD") != nullptr;  // time the forward (attn_fwd_kernel) instead
   mf_attention_fwd(qkv, 3 * D, o, D, lse, L, N, L, H, causal, 0);
   for (int rep = 0; rep < 5 && fwd; ++rep) {
-    hipMemset(st, 0, (size_t)NH * 64 * 8);
+    hipMemset(st, 0, nst * 8);
     mf_attention_fwd(qkv, 3 * D, o, D, lse, L, N, L, H, causal, 0);
     hipDeviceSynchronize();
   }
