@@ -20,6 +20,10 @@ int main(int argc, char** argv) {
   if (tile == 2) BN = 64;
   if (tile == 3) BM = BN = 64;
   if (tile >= 20) { BM = tile == 23 || tile == 24 ? 128 : 256; BN = (tile == 20 || tile == 23) ? 256 : 128; }
+  if (tile == 10) { BM = 160; BN = 128; }
+  if (tile == 15) { BM = 96; BN = 128; }
+  if (tile == 16) { BM = 160; BN = 64; }
+  if (tile == 26) { BM = 96; BN = 64; }
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   _Float16 *A, *B, *C, *bias, *aux;
   hipMalloc(&A, (size_t)M * K * 2); hipMalloc(&B, (size_t)N * K * 2); hipMalloc(&C, (size_t)M * N * 2);
