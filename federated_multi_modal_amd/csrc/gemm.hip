@@ -725,28 +725,21 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     else
       tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
   }
-  // tile ids: the ones the heuristic picks plus the sweep candidates kept for A/B (gemm_bench.py); the
-  // sweep also covered 192x128, 128x160, 160x160, 224x128, 96x192, 64x128, 160x192, 192x192 (slower)
+  // tile ids: the ones the heuristic picks (1, 2, 3, 10, 15, 16, 20, 26), plus 11 (160x128 with a
+  // 3-stage ring) and 21 (8-wave 256x128) as A/B baselines (tests/diagnostics/gemm_bench.py); the
+  // sweep also covered 128x192, 192x128, 128x160, 160x160, 224x128, 96x192, 64x128, 160x192, 192x192,
+  // 256x128 on 4 waves and 128x256 / 128x128 on 8 waves (slower on every MaPLe shape)
   switch (tile) {
     case 1: return launch_tile<128, 128, 2, 2, 2>(a, epilogue, st);
     case 2: return launch_tile<128, 64, 2, 2, 2>(a, epilogue, st);
     case 3: return launch_tile<64, 64, 2, 2, 2>(a, epilogue, st);
-    case 4: return launch_tile<256, 128, 4, 2, 2>(a, epilogue, st);
-    case 6: return launch_tile<128, 128, 2, 2, 3>(a, epilogue, st);
-    case 7: return launch_tile<128, 64, 2, 2, 3>(a, epilogue, st);
-    case 8: return launch_tile<128, 192, 2, 2, 3>(a, epilogue, st);
-    case 9: return launch_tile<128, 192, 2, 2, 2>(a, epilogue, st);
     case 10: return launch_tile<160, 128, 2, 2, 2>(a, epilogue, st);
     case 11: return launch_tile<160, 128, 2, 2, 3>(a, epilogue, st);
     case 15: return launch_tile<96, 128, 2, 2, 2>(a, epilogue, st);
     case 16: return launch_tile<160, 64, 2, 2, 2>(a, epilogue, st);
-    case 19: return launch_tile<128, 96, 2, 2, 2>(a, epilogue, st);
     case 26: return launch_tile<96, 64, 2, 2, 2>(a, epilogue, st);
     case 20: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 256, 2, 4>(a, epilogue, st);
     case 21: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 2, 4>(a, epilogue, st);
-    case 22: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 4, 2>(a, epilogue, st);
-    case 23: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<128, 256, 2, 4>(a, epilogue, st);
-    case 24: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<128, 128, 2, 4>(a, epilogue, st);
     default: return mf_set_error("mf_gemm: bad tile id", -2);
   }
 }

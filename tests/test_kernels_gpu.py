@@ -31,14 +31,9 @@ def assert_ulps(out, ref, max_ulp=1.0, frac=1e-2, what="", floor=2e-5):
 
 @pytest.mark.parametrize("M,N,K,tile", [(796, 2304, 768, 0), (6368, 768, 3072, 0), (770, 512, 2048, 1),
                                         (130, 44, 64, 3), (257, 1536, 512, 2), (6368, 3072, 768, 0),
-                                        # 8-wave phase-pipelined family (tiles 20-24), ragged M / N
+                                        # 8-wave phase-pipelined family (tiles 20, 21), ragged M / N
                                         (6368, 2304, 768, 20), (1000, 760, 192, 20), (6368, 3072, 768, 21),
-                                        (300, 388, 64, 21), (6368, 768, 3072, 22), (777, 132, 128, 22),
-                                        (2926, 1536, 512, 23), (129, 260, 320, 23), (2926, 512, 2048, 24),
-                                        (65, 36, 64, 24),
-                                        # 128x192 (tiles 8, 9), ragged M / N
-                                        (6368, 768, 3072, 8), (300, 200, 128, 8), (6368, 768, 768, 9),
-                                        (131, 388, 192, 9),
+                                        (300, 388, 64, 21), (777, 132, 128, 21), (129, 260, 320, 20),
                                         # 160x128 (tiles 10, 11)
                                         (6368, 768, 3072, 10), (333, 136, 128, 10), (6368, 768, 2304, 11),
                                         (170, 260, 192, 11),
@@ -132,7 +127,7 @@ def _gelu16(f):
     return (f.float() * t2.float()).half()
 
 
-@pytest.mark.parametrize("tile", [0, 8, 20, 22])
+@pytest.mark.parametrize("tile", [0, 10, 15, 20, 21])
 def test_gemm_epilogues(dev, tile):
     torch.manual_seed(0)
     M, N, K = 600, 1024, 256
