@@ -44,7 +44,35 @@ struct GemmArgs {
   int M, N, K;
   int vec8;    // C / aux row strides are multiples of 8 elements -> 16-byte epilogue accesses
   int ksplit;  // > 0: split-K slice of ksplit (multiple of 64) per blockIdx.z, fp32 partial at C + z*M*ldc
+  int xb;      // log2 of the N-range count of the XCD blocking (tile_of); 0: M-ranges only
 };
+
+// Tile of position p (0 .. tiles_m*tiles_n-1) in the XCD-blocked order.  The bijective remap below gives
+// each XCD a contiguous range of positions, and the positions enumerate 8 blocks, block x = M-range
+// (x >> xb) of 8 >> xb  x  N-range (x & (2^xb - 1)) of 2^xb, each block's tiles M-major (N inner).  So an
+// XCD's L2 holds one block: its A panels and B panels are each re-read by the tiles of the block only.
+// With xb = 0 an XCD takes whole rows of tiles (every B panel: the full weight matrix); for products
+// whose weight matrix exceeds an XCD's 4 MB L2 (N x K x 2 B at N = 3072, K = 768) splitting N too keeps
+// the working set of the XCD's concurrently running tiles inside its L2 (the host picks xb).
+MF_DEV void tile_of(int p, int tiles_m, int tiles_n, int xb, int& mt, int& nt) {
+  const int nb = 1 << xb, ma = 8 >> xb;
+  int off = 0;
+#pragma unroll 1
+  for (int x = 0; x < 8; ++x) {
+    const int ia = x >> xb, jb = x & (nb - 1);
+    const int m_lo = tiles_m * ia / ma, m_hi = tiles_m * (ia + 1) / ma;
+    const int n_lo = tiles_n * jb / nb, n_hi = tiles_n * (jb + 1) / nb;
+    const int sz = (m_hi - m_lo) * (n_hi - n_lo);
+    if (p < off + sz) {
+      const int loc = p - off, w = n_hi - n_lo;
+      mt = m_lo + loc / w;
+      nt = n_lo + loc % w;
+      return;
+    }
+    off += sz;
+  }
+  mt = nt = 0;  // unreachable for p < tiles_m * tiles_n
+}
 
 // Elementwise epilogue on 8 consecutive columns (fp16 staged value t = the GEMM result rounded at
 // the reference's first rounding point: fp16(acc + bias) or fp16(acc)).  The global operand an
@@ -337,8 +365,10 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g0) {
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int m0 = (wgid / tiles_n) * BM;
-  const int n0 = (wgid % tiles_n) * BN;
+  int mt, nt;
+  tile_of(wgid, (g.M + BM - 1) / BM, tiles_n, g.xb, mt, nt);
+  const int m0 = mt * BM;
+  const int n0 = nt * BN;
 
   // per-operand LDS-DMA: byte offset of this lane's 16 B for instruction i at k0 = 0 (all offsets in
   // the VGPR offset: the descriptor's range check covers it), and the instruction's LDS destination
@@ -472,8 +502,10 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int m0 = (wgid / tiles_n) * BM;
-  const int n0 = (wgid % tiles_n) * BN;
+  int mt, nt;
+  tile_of(wgid, (g.M + BM - 1) / BM, tiles_n, g.xb, mt, nt);
+  const int m0 = mt * BM;
+  const int n0 = nt * BN;
 
   // LDS-DMA: instruction covers 16 rows x 64 B; lane l -> row (l >> 2), chunk (l & 3), whose source
   // chunk is pre-swizzled; rows past M (N) read as zero through the buffer descriptor's range (every
@@ -654,6 +686,21 @@ inline int gemm_rule() {
   return r;
 }
 
+// XCD blocking (tile_of): the N-range count 2^xb minimising one XCD's operand footprint A/(8/2^xb) +
+// B/2^xb (bytes of the A rows and B rows it reads); MAPFED_GEMM_XB overrides (A/B knob, -1 = auto)
+inline int gemm_xcd_split(int M, int N, int K) {
+  static const int forced = getenv("MAPFED_GEMM_XB") ? atoi(getenv("MAPFED_GEMM_XB")) : -1;
+  if (forced >= 0) return std::min(forced, 3);
+  const double a_bytes = 2.0 * M * K, b_bytes = 2.0 * N * K;
+  int best = 0;
+  double best_fp = 1e300;
+  for (int xb = 0; xb <= 3; ++xb) {
+    const double fp = a_bytes / (8 >> xb) + b_bytes / (1 << xb);
+    if (fp < best_fp * 0.999) best = xb, best_fp = fp;
+  }
+  return best;
+}
+
 // automatic split count (tests/diagnostics/splitk_bench.py on the MaPLe dW shapes, K = 2926..6368):
 // >= 144 128x128 tiles run best unsplit; 64..143 tiles on 4 slices; fewer on 8
 inline int splitk_auto(int64_t tiles) { return tiles >= 144 ? 1 : (tiles >= 64 ? 4 : 8); }
@@ -705,7 +752,7 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
   const int vec8 = (ldc % 8 == 0) && (ld_aux % 8 == 0) && ((uintptr_t)C % 16 == 0) &&
                    (!aux_in || (uintptr_t)aux_in % 16 == 0) && (!aux_out || (uintptr_t)aux_out % 16 == 0);
   GemmArgs a{(const f16*)A, (const f16*)B, C, (const f16*)bias, (const f16*)aux_in, (f16*)aux_out,
-             lda, ldb, ldc, ld_aux, M, N, K, vec8, 0};
+             lda, ldb, ldc, ld_aux, M, N, K, vec8, 0, gemm_xcd_split(M, N, K)};
   hipStream_t st = (hipStream_t)stream;
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   if (a_kmajor || b_kmajor) {
@@ -774,7 +821,7 @@ extern "C" int mf_gemm_splitk(const void* A, int64_t lda, int a_kmajor, const vo
   splits = (K + ks - 1) / ks;
   if ((int64_t)splits * M * N > ws_floats) return mf_set_error("mf_gemm_splitk: workspace too small", -1);
   hipStream_t st = (hipStream_t)stream;
-  GemmArgs a{(const f16*)A, (const f16*)B, ws, nullptr, nullptr, nullptr, lda, ldb, (int64_t)N, 0, M, N, K, 1, ks};
+  GemmArgs a{(const f16*)A, (const f16*)B, ws, nullptr, nullptr, nullptr, lda, ldb, (int64_t)N, 0, M, N, K, 1, ks, 0};
   int rc;
   if (a_kmajor && b_kmajor) rc = launch_tile<128, 128, 2, 2, 2, true, true>(a, EPI_F32, st);
   else if (a_kmajor) rc = launch_tile<128, 128, 2, 2, 2, true, false>(a, EPI_F32, st);
