@@ -31,6 +31,7 @@ sys.path.insert(0, str(ROOT))
 
 from federated_multi_modal_amd import ops  # noqa: E402
 from federated_multi_modal_amd import synthetic as syn  # noqa: E402
+from federated_multi_modal_amd.captions import caption_tokens, draw_caption_weights  # noqa: E402
 from federated_multi_modal_amd.engine import EngineConfig, MapleEngine  # noqa: E402
 from federated_multi_modal_amd.federated import FedAvgBucket  # noqa: E402
 
@@ -162,6 +163,7 @@ def main():
     ap.add_argument("--roofline-kernel", default="gemm", choices=["gemm", "attention_fwd"])
     ap.add_argument("--no-eot-mode", action="store_true", help="skip the separately reported EOT-truncated run")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (K=1000 text side) side metric")
+    ap.add_argument("--no-caption-mode", action="store_true", help="skip the caption-batch (K19) side metric")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -281,6 +283,52 @@ def main():
                               "summation order (tests/test_engine_gpu.py::test_eot_truncated_text_tower_matches_full)"}
         del graph_t, eng_t, fed_t
         torch.cuda.synchronize()
+
+    # ---------------- caption-conditioned batches (K19), reported beside `value`:
+    # the caption fork's loaders attach captions to every batch, and the reference then grows the vision
+    # sequence by B rows per prompted layer (199 -> 455 at B = 32, J = 9).  Same protocol as the EOT mode;
+    # one draw of the random pooling / projection weights for the whole run (the reference draws them per
+    # forward on the host side; the device work per step is the same).
+    cap_mode = None
+    if not args.no_caption_mode:
+        eng_c = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed, captions=True),
+                            device=dev)
+        eng_c.set_lr(0.0026)
+        eng_c.set_captions(caption_tokens(syn.synthetic_captions(seed, rank, 0, B)),
+                           draw_caption_weights(torch.Generator().manual_seed(1000 * seed + rank)))
+
+        def load_c(i):
+            img, lab = batches[i % 2]
+            eng_c.img_in.copy_(img)
+            eng_c.label_in.copy_(lab)
+
+        load_c(0)
+        eng_c.train_step()
+        graph_c = eng_c.capture_train_step()
+        for i in range(args.warmup):
+            load_c(i)
+            graph_c.replay()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for i in range(args.steps):
+            load_c(i)
+            graph_c.replay()
+        torch.cuda.synchronize()
+        el_c = time.perf_counter() - a
+        if world > 1:
+            t = torch.tensor([el_c], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_c = float(t.item())
+        cap_mode = {"value": world * B * args.steps / el_c, "unit": "images/s",
+                    "ms_per_step": 1e3 * el_c / args.steps, "vision_rows_per_layer": list(eng_c.vis.Ls),
+                    "loss": eng_c.loss(),
+                    "parity": "tests/test_captions_gpu.py (reference caption fixtures: loss bit-identical, "
+                              "growing block outputs within the fp16 floor)"}
+        del graph_c, eng_c
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
 
     # ---------------- FedAvg alone (round-end cost), median of 5
     fts = []
@@ -468,6 +516,7 @@ def main():
         "fedavg_bucket_mb": 4.0 * (eng.n16 + eng.n32 + 1) / 1e6,
         "fedavg_valid_clients": fed.n_valid(),
         "eot_truncated_mode": eot_mode,
+        "caption_mode": cap_mode,
         "c5_side": c5,
         "eval_images_per_s": {"text_reencoded_per_batch": eval_full, "text_cached_per_pass": eval_cached,
                               "per_gpu": True},

@@ -20,7 +20,7 @@ if [ "${BENCH:-1}" = "1" ]; then
 fi
 if [ "${PROFILE:-1}" = "1" ]; then
   timeout -k 10 ${PROF_TIMEOUT:-400} rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof -o run -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-eot-mode --no-c5 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-eot-mode --no-c5 --no-caption-mode ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -2 gpurun_out/prof.log
   [ $rc -eq 0 ] || exit $rc
 fi
