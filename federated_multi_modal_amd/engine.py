@@ -387,7 +387,7 @@ class MapleEngine:
             # copies for the reference's state-dict key set; the table is generated on first use when the
             # weights are the seeded synthetic CLIP
             ls = vals.get("clip_model2.logit_scale", math.log(1 / 0.07))
-            self.clip_logit_scale = torch.tensor(float(np.asarray(ls, dtype=np.float64).reshape(-1)[0]),
+            self.clip_logit_scale = torch.tensor(float(torch.as_tensor(ls).reshape(-1)[0].item()),
                                                  dtype=F32, device=self.device)
             tok = vals.get("clip_model2.token_embedding.weight")
             self._token_table = None if tok is None else torch.as_tensor(np.asarray(tok, dtype=np.float32))
