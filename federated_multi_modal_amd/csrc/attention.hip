@@ -348,8 +348,10 @@ MF_DEV void fwd4_tile(const f16* sK, const f16* sV, const int* koff, const int* 
 // Staging overlaps the first tile: its Q fragments are loaded first, then K, then V (LDS-DMA); the
 // scores start once Q and K have landed (vmcnt = this wave's V loads) and V is waited for only before
 // P.V, so the V transfer runs under the score MFMAs and the softmax.
-template <int LKP, bool CAUSAL>
-__global__ __launch_bounds__(1024) void attn_fwd4_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
+// MAXT = 512 for 257..512 rows: one workgroup per CU (K / V of the head take up to 128 KB of LDS), so
+// two waves per SIMD and a 256-VGPR budget for the LKP/4 register-resident scores per lane.
+template <int LKP, bool CAUSAL, int MAXT = 1024>
+__global__ __launch_bounds__(MAXT) void attn_fwd4_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
                                                            f16* __restrict__ out, int64_t ld_out,
                                                            float* __restrict__ lse, int ld_lse, int L, int H) {
   __shared__ __attribute__((aligned(16))) f16 sK[LKP * 64];
@@ -848,6 +850,36 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
   if (ld_lse < L || (ld_qkv % 8) || (ld_out % 4)) return mf_set_error("mf_attention_fwd: bad strides", -1);
   const int LP = padded_len(L);
   hipStream_t st = (hipStream_t)stream;
+  static const int fwd_variant = getenv("MAPFED_ATTN_FWD") ? atoi(getenv("MAPFED_ATTN_FWD")) : 4;  // A/B knob: 1 = attn_fwd_kernel
+  if (L > 256 && fwd_variant == 4) {
+    // register-resident scores at up to 512 keys: 8 waves (512 threads), 2 per SIMD, one workgroup per CU
+    const int qs4 = attn_qsplit(N * H, L), tiles = (L + 15) / 16;
+    const dim3 grid4(N * H, qs4), block4(64 * std::min(8, (tiles + qs4 - 1) / qs4));
+#define CALLF4L(P) \
+  attn_fwd4_kernel<P, false, 512><<<grid4, block4, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); break;
+    switch (tiles * 16) {
+      case 272: CALLF4L(272)
+      case 288: CALLF4L(288)
+      case 304: CALLF4L(304)
+      case 320: CALLF4L(320)
+      case 336: CALLF4L(336)
+      case 352: CALLF4L(352)
+      case 368: CALLF4L(368)
+      case 384: CALLF4L(384)
+      case 400: CALLF4L(400)
+      case 416: CALLF4L(416)
+      case 432: CALLF4L(432)
+      case 448: CALLF4L(448)
+      case 464: CALLF4L(464)
+      case 480: CALLF4L(480)
+      case 496: CALLF4L(496)
+      case 512: CALLF4L(512)
+      default: return mf_set_error("attention: bad padded length", -1);
+    }
+#undef CALLF4L
+    MF_CHECK_LAUNCH();
+    return 0;
+  }
   if (L > 256) {
     const dim3 grid(N * H, attn_qsplit(N * H, L)), block(attn_threads(L));
 #define CALLFL(P) attn_fwd_kernel<P, false><<<grid, block, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H);
@@ -856,7 +888,6 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
     MF_CHECK_LAUNCH();
     return 0;
   }
-  static const int fwd_variant = getenv("MAPFED_ATTN_FWD") ? atoi(getenv("MAPFED_ATTN_FWD")) : 4;  // A/B knob: 1 = attn_fwd_kernel
   if (fwd_variant == 4) {
     // the head's 16-query tiles split evenly over its workgroups (no workgroup without a tile)
     const int qs4 = attn_qsplit(N * H, L), tiles = (L + 15) / 16;
