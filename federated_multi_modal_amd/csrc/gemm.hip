@@ -626,6 +626,171 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   MF_STAMP(3);
 }
 
+
+// gemm8s: the 256x256 8-wave tile with the two wave rows (wm = 0, 1) staggered by one barrier (ping-pong,
+// cdna_hip_programming.md §5 "The 256² 8-phase template"): every phase is a memory section (fragment
+// ds_reads for this phase's MFMAs, one half-tile of LDS-DMA, the retire waits) and a compute section
+// (16 MFMAs), separated by barriers; wave row 1 runs one barrier behind row 0, so on each SIMD one wave
+// issues MFMAs while its partner loads.  Ring of 10 half-tile slots, half-tile H issued in the memory
+// section of phase H - 7.  With the stagger (derivation in DESIGN.md §6):
+//   RAW: a half-tile first read in phase f is retired (counted vmcnt) at the end of memory section f - 1;
+//   WAR: a slot last read in phase q is refilled in phase q + 2 or later (H - 10 is last read in phase
+//        <= H - 9, refilled in H - 7).
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm8s_kernel(GemmArgs g) {
+  constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NT = 512;
+  constexpr int WTM = BM / WM, WTN = BN / WN, QM = WTM / 2;
+  constexpr int QTM = QM / 16, TN = WTN / 16, TM = 2 * QTM;
+  constexpr int INS = 2;                 // LDS-DMA wave instructions per wave per half-tile (A and B alike)
+  constexpr int HK = 32;
+  constexpr int SLOT = 256 * HK;
+  constexpr int NSLOT = 10, E = 7;
+  constexpr int LDC = BN + 8;
+  constexpr int LDS_ELEMS = NSLOT * SLOT > BM * LDC ? NSLOT * SLOT : BM * LDC;
+  static_assert(LDS_ELEMS * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) f16 lds[LDS_ELEMS];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  int mt, nt;
+  tile_of(wgid, (g.M + BM - 1) / BM, tiles_n, g.xb, mt, nt);
+  const int m0 = mt * BM;
+  const int n0 = nt * BN;
+
+  const int src_chunk = (lane & 3) ^ ((-(lane >> 4)) & 3);
+  const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.A, 0, (int)(((int64_t)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t b_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.B, 0, (int)(((int64_t)(g.N - 1) * g.ldb + g.K) * 2), 0x00020000);
+  const int a_voff = ((lane >> 2) * (int)g.lda + src_chunk * 8) * 2;
+  const int b_voff = ((lane >> 2) * (int)g.ldb + src_chunk * 8) * 2;
+  auto slot = [&](int h) { return lds + (h % NSLOT) * SLOT; };
+  // issue half-tile H (K-tile H / 4; 0: A k0, 1: B k0, 2: A k1, 3: B k1)
+  auto issue = [&](int H) {
+    f16* dst = slot(H);
+    const int kofs = (H >> 2) * BK + HK * ((H >> 1) & 1);
+    if ((H & 1) == 0) {
+#pragma unroll
+      for (int i = 0; i < INS; ++i) {
+        const int row = (wid * INS + i) * 16;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(dst + row * HK), 16,
+                                                 a_voff + (int)(((int64_t)(m0 + row) * g.lda + kofs) * 2), 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < INS; ++i) {
+        const int row = (wid * INS + i) * 16;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_ptr_t)(dst + row * HK), 16,
+                                                 b_voff + (int)(((int64_t)(n0 + row) * g.ldb + kofs) * 2), 0, 0, 0);
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fg = lane >> 4;
+  const int frag_off = fr * HK + ((fg ^ ((-(fr >> 2)) & 3)) << 3);
+  auto read_a = [&](f16x8 (&af)[QTM], const f16* img, int mh) {
+#pragma unroll
+    for (int i = 0; i < QTM; ++i) af[i] = *(const f16x8*)(img + (wm * WTM + mh * QM + i * 16) * HK + frag_off);
+  };
+  auto read_b = [&](f16x8 (&bf)[TN], const f16* img) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bf[j] = *(const f16x8*)(img + (wn * WTN + j * 16) * HK + frag_off);
+  };
+  auto mma = [&](const f16x8 (&af)[QTM], const f16x8 (&bf)[TN], int mh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < QTM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[mh * QTM + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[mh * QTM + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = g.K / BK;  // >= 2
+  const int nh = 4 * nk;
+  // prologue: half-tiles 0 .. 6 (nk >= 2: 8 exist), retire 0 and 1 (first read in phase 0)
+#pragma unroll
+  for (int h = 0; h < E; ++h) issue(h);
+  wait_vmcnt<INS * (E - 2)>();
+  lds_barrier();
+  if (wm == 1) lds_barrier();  // the stagger
+  f16x8 fx[QTM], fy[QTM], fb0[TN], fb1[TN];
+
+  // one K-tile; MODE 0: steady (issues half-tiles 4kt+7 .. 4kt+10), 1: kt = nk-2 (issues 4nk-1 only),
+  // 2: kt = nk-1 (none).  Retire counts = INS x half-tiles issued after the retired ones.
+  auto ktile = [&](int kt, auto mode_tag) {
+    constexpr int MODE = decltype(mode_tag)::value;
+    const int h0 = 4 * kt;
+    // phase 0 (m-half 0, k-sub 0)
+    read_a(fx, slot(h0), 0);
+    read_b(fb0, slot(h0 + 1));
+    if constexpr (MODE <= 1) issue(h0 + E);
+    lds_barrier();
+    mma(fx, fb0, 0);
+    lds_barrier();
+    // phase 1 (m-half 1, k-sub 0); retire half-tiles h0+2, h0+3 (first read in phase 2)
+    read_a(fy, slot(h0), 1);
+    if constexpr (MODE == 0) issue(h0 + E + 1);
+    if constexpr (MODE == 0) wait_vmcnt<INS * 5>();
+    else if constexpr (MODE == 1) wait_vmcnt<INS * 4>();
+    else wait_vmcnt<0>();
+    lds_barrier();
+    mma(fy, fb0, 1);
+    lds_barrier();
+    // phase 2 (m-half 1, k-sub 1)
+    read_a(fx, slot(h0 + 2), 1);
+    read_b(fb1, slot(h0 + 3));
+    if constexpr (MODE == 0) issue(h0 + E + 2);
+    lds_barrier();
+    mma(fx, fb1, 1);
+    lds_barrier();
+    // phase 3 (m-half 0, k-sub 1); retire half-tiles h0+4, h0+5 (first read in the next K-tile's phase 0)
+    read_a(fy, slot(h0 + 2), 0);
+    if constexpr (MODE == 0) issue(h0 + E + 3);
+    if constexpr (MODE == 0) wait_vmcnt<INS * 5>();
+    else if constexpr (MODE == 1) wait_vmcnt<INS * 2>();
+    lds_barrier();
+    mma(fy, fb1, 0);
+    lds_barrier();
+  };
+  for (int kt = 0; kt < nk - 2; ++kt) ktile(kt, std::integral_constant<int, 0>{});
+  ktile(nk - 2, std::integral_constant<int, 1>{});
+  ktile(nk - 1, std::integral_constant<int, 2>{});
+  (void)nh;
+  if (wm == 0) lds_barrier();  // even out the barrier count
+  __syncthreads();
+  epilogue_store<BM, BN, NT, TM, TN, EPI>(g, lds, acc, m0, n0, wm * WTM, wn * WTN, tid, fr, fg);
+}
+
+int launch_tile8s(const GemmArgs& a, int epi, hipStream_t st) {
+  const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  dim3 grid(tiles), block(512);
+  switch (epi) {
+    case EPI_NONE: gemm8s_kernel<EPI_NONE><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS: gemm8s_kernel<EPI_BIAS><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_RESID: gemm8s_kernel<EPI_BIAS_RESID><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_GELU: gemm8s_kernel<EPI_BIAS_GELU><<<grid, block, 0, st>>>(a); break;
+    case EPI_DGELU: gemm8s_kernel<EPI_DGELU><<<grid, block, 0, st>>>(a); break;
+    case EPI_F32: gemm8s_kernel<EPI_F32><<<grid, block, 0, st>>>(a); break;
+    case EPI_RESID: gemm8s_kernel<EPI_RESID><<<grid, block, 0, st>>>(a); break;
+    default: return mf_set_error("mf_gemm_nt: bad epilogue", -2);
+  }
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int BM, int BN, int WM, int WN>
 int launch_tile8(const GemmArgs& a, int epi, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
@@ -762,7 +927,7 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
   if (tile == 0) {  // heuristic: fill the 256 CUs (measured: tests/diagnostics/gemm_bench.py, gemm_stamps.cpp)
     const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
     if (t256 >= 192 && t256 <= 256 && K >= 512)
-      tile = 20;  // one round of 256x256 tiles on one workgroup per CU (vision QKV: 225 tiles)
+      tile = 20;  // one round of 256x256 tiles on one workgroup per CU (vision QKV: 225 tiles), gemm8s
     else if (M >= 4096 && K >= 512)  // vision products (M = 6368), tests/diagnostics/gemm_bench.py:
       // N = 3072: 160x128 (960 tiles); N = 768: 96x128 (402 tiles, two workgroups per CU) for K >= 2048,
       // 160x64 (480 tiles) for K = 768; +6..37 % over the 128-row tiles
@@ -772,8 +937,9 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     else
       tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
   }
-  // tile ids: the ones the heuristic picks (1, 2, 3, 10, 15, 16, 20, 26), plus 11 (160x128 with a
-  // 3-stage ring) and 21 (8-wave 256x128) as A/B baselines (tests/diagnostics/gemm_bench.py); the
+  // tile ids: the ones the heuristic picks (1, 2, 3, 10, 15, 16, 20 = gemm8s, 26), plus 11 (160x128 with a
+  // 3-stage ring), 21 (8-wave 256x128) and 22 (the unstaggered gemm8 at 256x256) as A/B baselines
+  // (tests/diagnostics/gemm_bench.py); the
   // sweep also covered 128x192, 192x128, 128x160, 160x160, 224x128, 96x192, 64x128, 160x192, 192x192,
   // 256x128 on 4 waves and 128x256 / 128x128 on 8 waves (slower on every MaPLe shape)
   switch (tile) {
@@ -785,8 +951,9 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     case 15: return launch_tile<96, 128, 2, 2, 2>(a, epilogue, st);
     case 16: return launch_tile<160, 64, 2, 2, 2>(a, epilogue, st);
     case 26: return launch_tile<96, 64, 2, 2, 2>(a, epilogue, st);
-    case 20: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 256, 2, 4>(a, epilogue, st);
+    case 20: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8s(a, epilogue, st);
     case 21: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 2, 4>(a, epilogue, st);
+    case 22: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 256, 2, 4>(a, epilogue, st);
     default: return mf_set_error("mf_gemm: bad tile id", -2);
   }
 }

@@ -2,7 +2,9 @@
 text M = 38*77), against hipBLASLt (torch.mm, plain product, no epilogue) as a yardstick, and check
 each tile configuration against a torch fp32 matmul.  Prints TFLOP/s.
 
-    python gemm_bench.py [tiles]        tiles: comma list of mf_gemm_nt tile ids (0 = heuristic)
+    python gemm_bench.py [tiles] [big]  tiles: comma list of mf_gemm_nt tile ids (0 = heuristic);
+                                        big: square 4096^3 / 8192^3 products instead of the step's shapes
+                                        (the guide's long-K yardstick for the main loop alone)
 
 A "!" marks a tile whose plain product misses the fp32 reference, "~" one whose output (with the
 shape's epilogue) is not bit-identical to the first listed tile's.
@@ -55,7 +57,11 @@ def main():
     print(f"{'shape':10s} {'blasLt':>8s} " + " ".join(f"{'t' + str(t):>8s}" for t in tiles) + "   (TFLOP/s; "
           "last col: us/step at heuristic tile)", flush=True)
     tot_us, tot_blas = 0.0, 0.0
-    for name, M, N, K, epi, calls in SHAPES:
+    shapes = SHAPES
+    if len(sys.argv) > 2 and sys.argv[2] == "big":
+        shapes = [("4096^3", 4096, 4096, 4096, ops.EPI_NONE, 1), ("8192^3", 8192, 8192, 8192, ops.EPI_NONE, 1),
+                  ("v.fc K4k", 6368, 3072, 4096, ops.EPI_NONE, 1), ("v.qkv K3k", 6368, 2304, 3072, ops.EPI_NONE, 1)]
+    for name, M, N, K, epi, calls in shapes:
         A = torch.randn(M, K, device=dev).half()
         B = (torch.randn(N, K, device=dev) * K ** -0.5).half()
         bias = torch.randn(N, device=dev).half() * 0.1
@@ -94,6 +100,8 @@ def main():
             res.append(f"{fl / us / 1e6:7.0f}{'' if ok else '!'}{'' if same else '~'}")
         print(f"{name:10s} {fl / ub / 1e6:8.0f} " + " ".join(f"{r:>8s}" for r in res), flush=True)
     print(f"sum over a c4 step: ours (tile {tiles[0]}) {tot_us / 1e3:.2f} ms, hipBLASLt plain {tot_blas / 1e3:.2f} ms")
+    if shapes is not SHAPES:
+        return
     # K-major operand forms (dX = dY . W with W read as [out][in]; dW = dY^T X read in place)
     print("K-major forms (TFLOP/s): NN = B K-major, TN = both K-major", flush=True)
     for name, M, N, K, epi, ak, bk in [("v.dfc NN", 6368, 3072, 768, ops.EPI_DGELU, False, True),

@@ -29,11 +29,26 @@ def assert_ulps(out, ref, max_ulp=1.0, frac=1e-2, what="", floor=2e-5):
     assert bad <= frac, f"{what}: {bad:.4f} of elements beyond half an ulp"
 
 
+@pytest.mark.parametrize("M,N,K", [(6368, 2304, 768), (513, 700, 256), (300, 516, 128)])
+def test_gemm8_staggered_matches_unstaggered(dev, M, N, K):
+    """The ping-pong 256x256 kernel (tile 20) issues every accumulator's MFMAs in the same k order as
+    the unstaggered one (tile 22): outputs bit-identical."""
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + K)
+    A = torch.randn(M, K, generator=g).half().to(dev)
+    B = (torch.randn(N, K, generator=g) * K ** -0.5).half().to(dev)
+    b = (torch.randn(N, generator=g) * 0.1).half().to(dev)
+    C20 = ops.gemm_nt(A, B, bias=b, epilogue=ops.EPI_BIAS, tile=20)
+    C22 = ops.gemm_nt(A, B, bias=b, epilogue=ops.EPI_BIAS, tile=22)
+    assert torch.equal(C20, C22)
+
+
 @pytest.mark.parametrize("M,N,K,tile", [(796, 2304, 768, 0), (6368, 768, 3072, 0), (770, 512, 2048, 1),
                                         (130, 44, 64, 3), (257, 1536, 512, 2), (6368, 3072, 768, 0),
-                                        # 8-wave phase-pipelined family (tiles 20, 21), ragged M / N
+                                        # 8-wave phase-pipelined family (tiles 20 = staggered 256x256, 21,
+                                        # 22 = unstaggered 256x256), ragged M / N, K down to two K-tiles
                                         (6368, 2304, 768, 20), (1000, 760, 192, 20), (6368, 3072, 768, 21),
                                         (300, 388, 64, 21), (777, 132, 128, 21), (129, 260, 320, 20),
+                                        (300, 516, 128, 20), (6368, 2304, 768, 22), (129, 260, 320, 22),
                                         # 160x128 (tiles 10, 11)
                                         (6368, 768, 3072, 10), (333, 136, 128, 10), (6368, 768, 2304, 11),
                                         (170, 260, 192, 11),
