@@ -928,12 +928,18 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
     if (t256 >= 192 && t256 <= 256 && K >= 512)
       tile = 20;  // one round of 256x256 tiles on one workgroup per CU (vision QKV: 225 tiles), gemm8s
+    else if (M >= 16384 && K >= 512)  // the C5 text tower (M = 77 000): many rounds of tiles whatever the
+      // shape, so the tile's own efficiency decides (gemm_bench.py ... c5): 256x256 for N >= 2048, 160x128
+      // otherwise (+6..40 % over the M = 6368 picks on the N = 512 products)
+      tile = N >= 2048 ? 20 : 10;
     else if (M >= 4096 && K >= 512)  // vision products (M = 6368), tests/diagnostics/gemm_bench.py:
       // N = 3072: 160x128 (960 tiles); N = 768: 96x128 (402 tiles, two workgroups per CU) for K >= 2048,
       // 160x64 (480 tiles) for K = 768; +6..37 % over the 128-row tiles
       tile = (N > 1024 || gemm_rule() == 1) ? 10 : (K >= 2048 ? 15 : 16);
     else if (M >= 2048 && N >= 1024 && K <= 768 && gemm_rule() != 1)
       tile = N >= 2048 ? 15 : 26;  // text (M = 2926): c_fc and its dX on 96x128, QKV on 96x64
+    else if (M >= 2048 && N <= 768 && K >= 512 && gemm_rule() != 1)
+      tile = 26;  // text N = 512 products (out-proj, c_proj, their dX, dQKV): 96x64, 248 tiles, +5..20 % over 64x64
     else
       tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
   }

@@ -4,7 +4,8 @@ each tile configuration against a torch fp32 matmul.  Prints TFLOP/s.
 
     python gemm_bench.py [tiles] [big]  tiles: comma list of mf_gemm_nt tile ids (0 = heuristic);
                                         big: square 4096^3 / 8192^3 products instead of the step's shapes
-                                        (the guide's long-K yardstick for the main loop alone)
+                                        (the guide's long-K yardstick for the main loop alone);
+                                        c5: the K = 1000 text tower's products (77 000 rows)
 
 A "!" marks a tile whose plain product misses the fp32 reference, "~" one whose output (with the
 shape's epilogue) is not bit-identical to the first listed tile's.
@@ -58,6 +59,12 @@ def main():
           "last col: us/step at heuristic tile)", flush=True)
     tot_us, tot_blas = 0.0, 0.0
     shapes = SHAPES
+    if len(sys.argv) > 2 and sys.argv[2] == "c5":  # the K = 1000 text tower (77 000 rows)
+        shapes = [("c5.qkv", 77000, 1536, 512, ops.EPI_BIAS, 12), ("c5.out", 77000, 512, 512, ops.EPI_BIAS_RESID, 12),
+                  ("c5.fc", 77000, 2048, 512, ops.EPI_BIAS_GELU, 12),
+                  ("c5.proj", 77000, 512, 2048, ops.EPI_BIAS_RESID, 12),
+                  ("c5.dfc", 77000, 2048, 512, ops.EPI_DGELU, 12), ("c5.dh", 77000, 512, 2048, ops.EPI_NONE, 12),
+                  ("c5.do", 77000, 512, 512, ops.EPI_NONE, 12), ("c5.dqkv", 77000, 512, 1536, ops.EPI_NONE, 12)]
     if len(sys.argv) > 2 and sys.argv[2] == "big":
         shapes = [("4096^3", 4096, 4096, 4096, ops.EPI_NONE, 1), ("8192^3", 8192, 8192, 8192, ops.EPI_NONE, 1),
                   ("v.fc K4k", 6368, 3072, 4096, ops.EPI_NONE, 1), ("v.qkv K3k", 6368, 2304, 3072, ops.EPI_NONE, 1)]
@@ -101,7 +108,7 @@ def main():
         print(f"{name:10s} {fl / ub / 1e6:8.0f} " + " ".join(f"{r:>8s}" for r in res), flush=True)
     print(f"sum over a c4 step: ours (tile {tiles[0]}) {tot_us / 1e3:.2f} ms, hipBLASLt plain {tot_blas / 1e3:.2f} ms")
     if shapes is not SHAPES:
-        return
+        return  # the sum line above is then over the listed shapes at the listed call counts
     # K-major operand forms (dX = dY . W with W read as [out][in]; dW = dY^T X read in place)
     print("K-major forms (TFLOP/s): NN = B K-major, TN = both K-major", flush=True)
     for name, M, N, K, epi, ak, bk in [("v.dfc NN", 6368, 3072, 768, ops.EPI_DGELU, False, True),
