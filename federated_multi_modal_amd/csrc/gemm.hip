@@ -845,7 +845,8 @@ int launch_kmajor(const GemmArgs& a, bool ta, bool tb, int epi, int tile, hipStr
 #undef MF_KM
 }
 
-// tile-rule A/B knob (MAPFED_GEMM_RULE=1: every vision product on 160x128, text on 128-row tiles)
+// tile-rule A/B knob (MAPFED_GEMM_RULE=1: every vision product on 160x128, text on 128-row tiles;
+// 2: the text N = 512 products back on 64x64; 3: the vision QKV on the unstaggered 256x256 kernel)
 inline int gemm_rule() {
   static const int r = getenv("MAPFED_GEMM_RULE") ? atoi(getenv("MAPFED_GEMM_RULE")) : 0;
   return r;
@@ -927,7 +928,7 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
   if (tile == 0) {  // heuristic: fill the 256 CUs (measured: tests/diagnostics/gemm_bench.py, gemm_stamps.cpp)
     const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
     if (t256 >= 192 && t256 <= 256 && K >= 512)
-      tile = 20;  // one round of 256x256 tiles on one workgroup per CU (vision QKV: 225 tiles), gemm8s
+      tile = gemm_rule() == 3 ? 22 : 20;  // one round of 256x256 tiles on one workgroup per CU (vision QKV: 225 tiles), gemm8s
     else if (M >= 16384 && K >= 512)  // the C5 text tower (M = 77 000): many rounds of tiles whatever the
       // shape, so the tile's own efficiency decides (gemm_bench.py ... c5): 256x256 for N >= 2048, 160x128
       // otherwise (+6..40 % over the M = 6368 picks on the N = 512 products)
@@ -938,7 +939,7 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
       tile = (N > 1024 || gemm_rule() == 1) ? 10 : (K >= 2048 ? 15 : 16);
     else if (M >= 2048 && N >= 1024 && K <= 768 && gemm_rule() != 1)
       tile = N >= 2048 ? 15 : 26;  // text (M = 2926): c_fc and its dX on 96x128, QKV on 96x64
-    else if (M >= 2048 && N <= 768 && K >= 512 && gemm_rule() != 1)
+    else if (M >= 2048 && N <= 768 && K >= 512 && gemm_rule() != 1 && gemm_rule() != 2)
       tile = 26;  // text N = 512 products (out-proj, c_proj, their dX, dQKV): 96x64, 248 tiles, +5..20 % over 64x64
     else
       tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 for r in $(seq 1 ${ROUNDS:-2}); do
   for v in ${VARIANTS:--}; do
     envs=""; [ "$v" != "-" ] && envs="${v//,/ }"
-    out=$(env $envs timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 --no-cpu-baseline --no-eot-mode 2> gpurun_out/ab.err)
+    out=$(env $envs timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 --no-cpu-baseline --no-eot-mode ${BENCH_ARGS:-} 2> gpurun_out/ab.err)
     rc=$?; [ $rc -eq 0 ] || { echo "variant $v rc=$rc"; tail -3 gpurun_out/ab.err; exit $rc; }
     echo "$v $(echo "$out" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"],1), "img/s", round(d["ms_per_step"],3), "ms")')"
   done

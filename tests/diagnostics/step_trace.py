@@ -1,6 +1,7 @@
-"""Diagnostic (GPU box): the c4 client step (no captions), hipGraph-replayed, for a rocprofv3 kernel
-trace whose timeline shows the step's idle gaps and stream overlap:
-    rocprofv3 --kernel-trace -d gpurun_out/trace -o run -- python3 tests/diagnostics/step_trace.py 5
+"""Diagnostic (GPU box): the c4 (or, with `c5`, the K = 1000-class) client step, no captions,
+hipGraph-replayed, for a rocprofv3 kernel trace whose timeline shows the step's idle gaps and stream
+overlap (rocprofv3's tracing serialises the two streams, so the per-kernel times are isolated ones):
+    rocprofv3 --kernel-trace -d gpurun_out/trace -o run -- python3 tests/diagnostics/step_trace.py 5 [c5]
 then `python tests/diagnostics/step_trace.py --analyze gpurun_out/trace/run_results.db` (CPU)."""
 import sys
 import time
@@ -49,7 +50,8 @@ if __name__ == "__main__":
     from federated_multi_modal_amd import synthetic as syn  # noqa: E402
     from federated_multi_modal_amd.engine import EngineConfig, MapleEngine  # noqa: E402
 
-    J, K, B, seed, steps = 9, 38, 32, 0, int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    J, B, seed, steps = 9, 32, 0, int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    K = 1000 if len(sys.argv) > 2 and sys.argv[2] == "c5" else 38
     dev = torch.device("cuda:0")
     e = MapleEngine(EngineConfig(batch=B, classnames=syn.synthetic_classnames(K, seed), prompt_depth=J, seed=seed),
                     device=dev)
@@ -65,4 +67,4 @@ if __name__ == "__main__":
         g.replay()
         torch.cuda.synchronize()
         time.sleep(0.002)
-    print(f"c4 step: last {1e3 * (time.perf_counter() - a):.2f} ms, loss {e.loss():.4f}")
+    print(f"K={K} step: last {1e3 * (time.perf_counter() - a):.2f} ms, loss {e.loss():.4f}")
