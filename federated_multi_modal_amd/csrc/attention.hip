@@ -593,8 +593,9 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_dq_kernel(const f16* __restri
 //   phase 1: wave w owns keys 32w..32w+31 (K, V fragments in registers) and sweeps the queries:
 //            S^T-ordered P = exp(S*scale - LSE), dS = P (dP - D); dV += P^T dO, dK += dS^T Q, and
 //            dS^T (fp16, the operand precision the dQ product uses) is written to LDS [key][q];
-//   phase 2: K replaces Q in LDS; wave w owns queries 32w..32w+31: dQ = dS K from the stored dS^T
-//            (no recompute of S and dP, no separate D kernel).
+//   phase 2: K replaces Q in LDS, written from the waves' K fragments (no second fetch of K); wave w
+//            owns queries 32w..32w+31: dQ = dS K from the stored dS^T (no recompute of S and dP, no
+//            separate D kernel).
 // LDS at LP = 224: Q 28 KB + dO 28 KB + dS^T 224 x 232 fp16 (101.5 KB) + LSE/D 1.75 KB = 159.25 KB.
 template <int LP>
 struct BwdLds {
@@ -635,7 +636,9 @@ __global__ __launch_bounds__(64 * (LP / (16 * KT))) void attn_bwd_fused_kernel(
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int fr = lane & 15, fg = lane >> 4;
-  // phase 0: D and LSE of queries 16*KT*w .. +16*KT-1 (LPQ lanes per query, 64/LPQ dims each)
+  // phase 0: D and LSE of queries 16*KT*w .. +16*KT-1 (LPQ lanes per query, 64/LPQ dims each), from
+  // global O and dO while the staging is in flight (reading dO back from LDS instead serialises D behind
+  // the staging: +0.4 us per workgroup, tests/diagnostics/attn_stamps.cpp)
   {
     constexpr int LPQ = 4 / KT, DPL = 64 / LPQ;
     const int q = 16 * KT * w + lane / LPQ;
@@ -755,8 +758,15 @@ __global__ __launch_bounds__(64 * (LP / (16 * KT))) void attn_bwd_fused_kernel(
   MF_ASTAMP(2);
   // ---- phase 2: K into the Q region; dQ for queries q0..q0+16*KT-1 from dS^T
   __syncthreads();  // dS^T complete, every wave done reading Q / dO
-  stage_rows<LP>(sQ, base, ld_qkv, L, D + h * 64);
-  stage_wait();
+  // the K image from the waves' own K fragments (rows k0.., the stage_rows layout: rows >= L hold row
+  // L - 1), instead of fetching K again
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    const int row = k0 + 16 * kt + fr;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) *(f16x8*)(sQ + row * 64 + (((4 * s2 + fg) ^ (row & 7)) << 3)) = kf[kt][s2];
+  }
+  __syncthreads();
   MF_ASTAMP(3);
   const f16* sK = sQ;
   const int q0 = 16 * KT * w;
@@ -952,7 +962,8 @@ extern "C" int mf_attention_bwd(const void* qkv, int64_t ld_qkv, const void* out
     MF_CHECK_LAUNCH();
     return 0;
   }
-  static const int bwd_variant = getenv("MAPFED_ATTN_BWD") ? atoi(getenv("MAPFED_ATTN_BWD")) : 2;  // A/B knob
+  // A/B knobs, read per call (host side only; a captured graph keeps the kernels it captured)
+  const int bwd_variant = getenv("MAPFED_ATTN_BWD") ? atoi(getenv("MAPFED_ATTN_BWD")) : 2;
   if (bwd_variant == 2 && LP <= 224) {
     static const int kt_w = getenv("MAPFED_ATTN_BWD_KT") ? atoi(getenv("MAPFED_ATTN_BWD_KT")) : 1;  // tuning knob
     const dim3 gridf(N * H), blockf(64 * (LP / (16 * kt_w)));

@@ -49,6 +49,7 @@ for (N, L, H, causal) in [(32, 199, 12, False), (38, 77, 8, True), (4, 199, 12, 
     ck = (out.view(torch.int16).long().sum().item(), lse.double().sum().item())
     tf = timeit(lambda: ops.attention_fwd(qkv, N, L, H, causal, out=out, lse=lse))
     tb = timeit(lambda: ops.attention_bwd(qkv, out, dout, lse, N, L, H, causal, dqkv=dqkv, ws=ws))
+    ckb = dqkv.view(torch.int16).long().sum().item()  # backward variants claiming bit-identity print the same
     fl_f = 4.0 * N * H * L * L * 64 * (0.5 if causal else 1.0)
     fl_b = 2.5 * fl_f  # QK^T, dP = dO V^T, dV = P^T dO, dQ, dK (5 products vs 2)
     by_f = 2.0 * 4 * N * L * D
@@ -56,4 +57,4 @@ for (N, L, H, causal) in [(32, 199, 12, False), (38, 77, 8, True), (4, 199, 12, 
     roof_f = min(2.5e15, fl_f / by_f * 8e12)
     print(f"N={N} L={L} H={H} causal={causal}: fwd {tf:7.1f}us {fl_f / tf / 1e6:6.0f} TF "
           f"{by_f / tf / 1e3:6.0f} GB/s frac(roof {roof_f / 1e12:.0f} TF)={fl_f / tf / 1e6 / (roof_f / 1e12):.3f} "
-          f"| bwd {tb:7.1f}us {fl_b / tb / 1e6:6.0f} TF {by_b / tb / 1e3:6.0f} GB/s | max err {err:.2e} ck {ck}", flush=True)
+          f"| bwd {tb:7.1f}us {fl_b / tb / 1e6:6.0f} TF {by_b / tb / 1e3:6.0f} GB/s | max err {err:.2e} ck {ck} ckb {ckb}", flush=True)

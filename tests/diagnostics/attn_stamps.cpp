@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
     hipDeviceSynchronize();
   }
   for (int rep = 0; rep < 5 && !fwd; ++rep) {
-    hipMemset(st, 0, (size_t)NH * 64);
+    hipMemset(st, 0, nst * 8);
     int rc = mf_attention_bwd(qkv, 3 * D, o, D, dout, D, lse, ws, L, dqkv, 3 * D, N, L, H, causal, 0);
     if (rc) { printf("error %s\n", mf_last_error()); return 1; }
     hipDeviceSynchronize();
@@ -74,22 +74,29 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
-  std::vector<unsigned long long> s((size_t)NH * 8);
+  // backward: the fused kernel (one workgroup per head) or, with STAMP_SPLIT=s, attn_bwd_split_kernel
+  // (MAPFED_ATTN_BWD=3 MAPFED_ATTN_BWD_SPLIT=s: s workgroups per head, id = head * s + split)
+  const int nwg = NH * (getenv("STAMP_SPLIT") ? atoi(getenv("STAMP_SPLIT")) : 1);
+  std::vector<unsigned long long> s((size_t)nwg * 8);
   hipMemcpy(s.data(), st, s.size() * 8, hipMemcpyDeviceToHost);
   unsigned long long t0 = ~0ull, t4 = 0;
-  for (int b = 0; b < NH; ++b) { t0 = std::min(t0, s[b * 8]); t4 = std::max(t4, s[b * 8 + 4]); }
+  for (int b = 0; b < nwg; ++b) { t0 = std::min(t0, s[b * 8]); t4 = std::max(t4, s[b * 8 + 4]); }
   auto us = [](unsigned long long d) { return d / 100.0; };
   const char* names[4] = {"stage+D", "phase1", "restage K", "phase2"};
-  printf("N=%d L=%d H=%d causal=%d: %d workgroups, span %.2f us\n", N, L, H, causal, NH, us(t4 - t0));
+  printf("N=%d L=%d H=%d causal=%d: %d workgroups, span %.2f us\n", N, L, H, causal, nwg, us(t4 - t0));
   for (int k = 0; k < 4; ++k) {
     std::vector<double> v;
-    for (int b = 0; b < NH; ++b) v.push_back(us(s[b * 8 + k + 1] - s[b * 8 + k]));
+    for (int b = 0; b < nwg; ++b) v.push_back(us(s[b * 8 + k + 1] - s[b * 8 + k]));
     std::sort(v.begin(), v.end());
     printf("  %-10s min %7.2f  med %7.2f  p90 %7.2f  max %7.2f us\n", names[k], v[0], v[v.size() / 2], v[v.size() * 9 / 10], v.back());
   }
-  std::vector<double> st0;
-  for (int b = 0; b < NH; ++b) st0.push_back(us(s[b * 8] - t0));
-  std::sort(st0.begin(), st0.end());
+  std::vector<double> st0, en, life;
+  for (int b = 0; b < nwg; ++b) {
+    st0.push_back(us(s[b * 8] - t0)); en.push_back(us(s[b * 8 + 4] - t0)); life.push_back(us(s[b * 8 + 4] - s[b * 8]));
+  }
+  std::sort(st0.begin(), st0.end()); std::sort(en.begin(), en.end()); std::sort(life.begin(), life.end());
   printf("  start      min %7.2f  med %7.2f  p90 %7.2f  max %7.2f us\n", st0[0], st0[st0.size() / 2], st0[st0.size() * 9 / 10], st0.back());
+  printf("  end        min %7.2f  med %7.2f  p90 %7.2f  max %7.2f us\n", en[0], en[en.size() / 2], en[en.size() * 9 / 10], en.back());
+  printf("  lifetime   min %7.2f  med %7.2f  p90 %7.2f  max %7.2f us\n", life[0], life[life.size() / 2], life[life.size() * 9 / 10], life.back());
   return 0;
 }
