@@ -869,7 +869,9 @@ inline int gemm_xcd_split(int M, int N, int K) {
 
 // automatic split count (tests/diagnostics/splitk_bench.py on the MaPLe dW shapes, K = 2926..6368):
 // >= 144 128x128 tiles run best unsplit; 64..143 tiles on 4 slices; fewer on 8
-inline int splitk_auto(int64_t tiles) { return tiles >= 144 ? 1 : (tiles >= 64 ? 4 : 8); }
+// split count of a K-major weight gradient by its 128x128 output-tile count (tests/diagnostics/splitk_bench.py,
+// r02: 144 tiles (block 11's c_fc / c_proj dW, K = 6368) 3 splits 52.7 us against 65 us single-pass)
+inline int splitk_auto(int64_t tiles) { return tiles >= 256 ? 1 : (tiles >= 128 ? 3 : (tiles >= 64 ? 4 : 8)); }
 
 // split-K combine: C[m][n] = sum_{s=0..S-1} ws[s][m][n] in that order (deterministic), fp16 or fp32 out.
 // 4 columns per thread (N % 4 == 0).

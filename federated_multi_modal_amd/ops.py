@@ -94,6 +94,12 @@ def _ld(t: torch.Tensor) -> int:
     return t.stride(0)
 
 
+def _gemm_bytes(M, N, K, C, aux=None, a_bytes=2, b_bytes=2) -> float:
+    """Algorithmic bytes of one GEMM launch: A and B read once, C written once (at its element size), and
+    the epilogue's aux operand (residual read, pre-activation written or read: M x N fp16) once."""
+    return a_bytes * M * K + b_bytes * N * K + C.element_size() * M * N + (2.0 * M * N if aux is not None else 0.0)
+
+
 def gemm_nt(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NONE, tile=0):
     """C[M,N] = epi(A[M,K] . B[N,K]^T)."""
     M, K = A.shape
@@ -105,7 +111,7 @@ def gemm_nt(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NON
     ld_aux = _ld(aux) if aux is not None else 0
     ev = None
     if _PROBE is not None and _PROBE.wants("gemm"):
-        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), _gkey())
+        ev = _PROBE.around(2.0 * M * N * K, _gemm_bytes(M, N, K, C, aux), _gkey())
     call("mf_gemm_nt", _p(A), _ld(A), _p(B), _ld(B), _p(C), _ld(C), M, N, K, _p(bias), _p(aux_in), _p(aux_out),
          ld_aux, epilogue, tile, _s())
     if ev is not None:
@@ -127,7 +133,7 @@ def gemm(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NONE, 
     ld_aux = _ld(aux) if aux is not None else 0
     ev = None
     if _PROBE is not None and _PROBE.wants("gemm"):
-        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), _gkey())
+        ev = _PROBE.around(2.0 * M * N * K, _gemm_bytes(M, N, K, C, aux), _gkey())
     call("mf_gemm", _p(A), _ld(A), int(a_kmajor), _p(B), _ld(B), int(b_kmajor), _p(C), _ld(C), M, N, K, _p(bias),
          _p(aux_in), _p(aux_out), ld_aux, epilogue, tile, _s())
     if ev is not None:
@@ -153,7 +159,7 @@ def gemm_splitk(A, B, C, ws, splits=0, a_kmajor=False, b_kmajor=False):
     assert ws.dtype == torch.float32 and C.dtype in (torch.float16, torch.float32)
     ev = None
     if _PROBE is not None and _PROBE.wants("gemm"):
-        ev = _PROBE.around(2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), _gkey())
+        ev = _PROBE.around(2.0 * M * N * K, _gemm_bytes(M, N, K, C), _gkey())
     call("mf_gemm_splitk", _p(A), _ld(A), int(a_kmajor), _p(B), _ld(B), int(b_kmajor), _p(C), _ld(C), M, N, K,
          _p(ws), ws.numel(), splits, int(C.dtype == torch.float16), _s())
     if ev is not None:
