@@ -432,8 +432,9 @@ def main():
     # (towers serialised on one stream here so that no other kernel runs inside a probed launch)
     probe = ops.KernelProbe({"gemm": "gemm", "attention_fwd": "attention"}[args.roofline_kernel])
     aprobe = ops.KernelProbe("attention") if args.roofline_kernel == "gemm" else probe
+    hprobe = ops.KernelProbe("hbm")  # the streaming kernels (LayerNorm, clip-grad-norm, SGD) against 8 TB/s
     eng.overlap_towers = False
-    for pr in dict.fromkeys((probe, aprobe)):  # the GEMM probe, then the attention probe (own steps)
+    for pr in dict.fromkeys((probe, aprobe, hprobe)):  # one probe at a time, each over its own two steps
         ops.set_probe(pr)
         for i in range(2):
             load(i)
@@ -455,6 +456,13 @@ def main():
         roof_t = min(MFMA_PEAK_F16, attn_roof[key]["flop_per_byte"] * HBM_PEAK)
         attn_roof[key]["roof_tflops"] = roof_t / 1e12
         attn_roof[key]["roof_frac"] = a["tflops"] * 1e12 / roof_t
+
+    # the HBM-bound kernels against 8 TB/s (algorithmic bytes per launch: ops._hbm call sites)
+    hbm_roof = {}
+    for key in hprobe.keys():
+        a = hprobe.summary(key)
+        hbm_roof[key] = {"launches_per_step": a["launches"] // 2, "avg_launch_us": a["avg_us"],
+                         "bytes_per_launch": a["bytes_per_launch"], "gbs": a["gbs"], "hbm_frac": a["gbs"] * 1e9 / HBM_PEAK}
 
     # HBM traffic of the dominant kernel family, per launch, from the rocprofv3 PMC passes of this same
     # command (scripts/gpu_pmc.sh -> profiles/*_<config>_pmc_summary.json: FETCH_SIZE doubled per
@@ -526,6 +534,7 @@ def main():
         "loss": loss,
         "roofline": roof,
         "attention_roofline": attn_roof,
+        "hbm_kernels": hbm_roof,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

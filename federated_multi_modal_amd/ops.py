@@ -100,6 +100,18 @@ def _gemm_bytes(M, N, K, C, aux=None, a_bytes=2, b_bytes=2) -> float:
     return a_bytes * M * K + b_bytes * N * K + C.element_size() * M * N + (2.0 * M * N if aux is not None else 0.0)
 
 
+def _hbm(key: str, nbytes: float):
+    """HIP-event probe around a streaming (HBM-bound) kernel: algorithmic bytes per launch."""
+    if _PROBE is not None and _PROBE.wants("hbm"):
+        return _PROBE.around(0.0, nbytes, key)
+    return None
+
+
+def _rec(ev):
+    if ev is not None:
+        ev.record()
+
+
 def gemm_nt(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NONE, tile=0):
     """C[M,N] = epi(A[M,K] . B[N,K]^T)."""
     M, K = A.shape
@@ -176,8 +188,11 @@ def layernorm_fwd(x, gamma, beta, y=None, mean=None, rstd=None, row_index=None):
         mean = torch.empty(rows, device=x.device, dtype=torch.float32)
     if rstd is None:
         rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+    # x read, y written (fp16), mean / rstd written (fp32)
+    ev = _hbm(f"layernorm_fwd/D{D}", rows * D * 4.0 + rows * 8.0)
     call("mf_layernorm_fwd", _p(x), _ld(x), _p(row_index), _p(gamma), _p(beta), _p(y), _ld(y), _p(mean), _p(rstd),
          rows, D, _s())
+    _rec(ev)
     return y, mean, rstd
 
 
@@ -185,8 +200,10 @@ def layernorm_fwd(x, gamma, beta, y=None, mean=None, rstd=None, row_index=None):
 def layernorm_fwd_inject(x, gamma, beta, y, mean, rstd, prompt, L, row0, nrows):
     """prompt_inject_fwd(x, prompt, ...) + layernorm_fwd(x, ...) in one kernel (bit-identical)."""
     rows, D = x.shape
+    ev = _hbm(f"layernorm_fwd/D{D}", rows * D * 4.0 + rows * 8.0)
     call("mf_layernorm_fwd_inject", _p(x), _ld(x), _p(gamma), _p(beta), _p(y), _ld(y), _p(mean), _p(rstd), rows, D,
          _p(prompt), L, row0, nrows, _s())
+    _rec(ev)
     return y, mean, rstd
 
 
@@ -229,9 +246,13 @@ class LNGradBatch:
             self.descs.append((w.data_ptr() + 4 * nblk * D, dbeta.data_ptr(), nblk, D))
             self.max_cols = max(self.max_cols, D)
             self.dev_descs = None
+        # dy, x (and the residual gradient) read, dx written (fp16); mean / rstd read; dgamma / dbeta partials
+        ev = _hbm(f"layernorm_bwd/D{D}", rows * D * (6.0 + (2.0 if dres is not None else 0.0)) + rows * 8.0
+                  + self.ws[key].numel() * 4.0)
         call("mf_layernorm_bwd", _p(dy), _ld(dy), _p(x), _ld(x), _p(row_index), _p(gamma), _p(mean), _p(rstd),
              _p(dres), _ld(dres) if dres is not None else 0, _p(dx), _ld(dx), None, None, _p(self.ws[key]), rows, D,
              0, _s())
+        _rec(ev)
         return dx
 
     def bwd_inject(self, dy, x, gamma, mean, rstd, dx, dgamma, dbeta, dres, prompt_grad, L, row0, nrows):
@@ -257,9 +278,12 @@ class LNGradBatch:
             self.descs.append((part.data_ptr(), prompt_grad.data_ptr(), n, nrows * D))
             self.max_cols = max(self.max_cols, nrows * D)
             self.dev_descs = None
+        ev = _hbm(f"layernorm_bwd/D{D}", rows * D * (6.0 + (2.0 if dres is not None else 0.0)) + rows * 8.0
+                  + (self.ws[key].numel() + self.ws[ikey].numel()) * 4.0)
         call("mf_layernorm_bwd_inject", _p(dy), _ld(dy), _p(x), _ld(x), _p(gamma), _p(mean), _p(rstd), _p(dres),
              _ld(dres) if dres is not None else 0, _p(dx), _ld(dx), _p(self.ws[key]), rows, D, _p(self.ws[ikey]), L,
              row0, nrows, _s())
+        _rec(ev)
         return dx
 
     def finish(self):
@@ -467,12 +491,17 @@ def optim_chunk_elems() -> int:
 
 
 def clip_grad_norm(g16, g32, chunks, nchunks, max_norm, part, out):
+    ev = _hbm("clip_grad_norm", g16.numel() * 2.0 + g32.numel() * 4.0)  # every gradient read once
     call("mf_clip_grad_norm", _p(g16), _p(g32), _p(chunks), nchunks, float(max_norm), _p(part), _p(out), _s())
+    _rec(ev)
 
 
 def sgd_step(p, g, buf, coef, hyper):
     """hyper: device fp32 tensor {lr, momentum, weight_decay, first_step}."""
+    # p, g, momentum read; p, momentum written (each at the parameter's element size)
+    ev = _hbm(f"sgd_step/{'f16' if p.dtype == torch.float16 else 'f32'}", p.numel() * 5.0 * p.element_size())
     call("mf_sgd_step", _p(p), _p(g), _p(buf), p.numel(), int(p.dtype == torch.float16), _p(coef), _p(hyper), _s())
+    _rec(ev)
 
 
 def fedavg_pack(p16, p32, invalid_flag, bucket):
