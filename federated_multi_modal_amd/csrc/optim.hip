@@ -31,13 +31,34 @@ __global__ void sumsq_chunks_kernel(const f16* __restrict__ g16, const float* __
                                     const Chunk* __restrict__ chunks, float* __restrict__ part) {
   const Chunk c = chunks[blockIdx.x];
   float s = 0.f;
+  // 16-byte loads over the chunk's 16-byte-aligned middle (the flat buffers are 256-B aligned), element
+  // loads for the ragged head and tail
   if (c.is16) {
-    for (int64_t i = c.start + threadIdx.x; i < c.end; i += blockDim.x) {
+    const int64_t a = min(c.end, (c.start + 7) & ~(int64_t)7), b = max(a, c.end & ~(int64_t)7);
+    for (int64_t i = c.start + threadIdx.x; i < a; i += blockDim.x) {
+      float v = (float)g16[i];
+      s += v * v;
+    }
+    for (int64_t i = a / 8 + threadIdx.x; i < b / 8; i += blockDim.x) {
+      const f16x8 v = ((const f16x8*)g16)[i];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += (float)v[e] * (float)v[e];
+    }
+    for (int64_t i = b + threadIdx.x; i < c.end; i += blockDim.x) {
       float v = (float)g16[i];
       s += v * v;
     }
   } else {
-    for (int64_t i = c.start + threadIdx.x; i < c.end; i += blockDim.x) {
+    const int64_t a = min(c.end, (c.start + 3) & ~(int64_t)3), b = max(a, c.end & ~(int64_t)3);
+    for (int64_t i = c.start + threadIdx.x; i < a; i += blockDim.x) {
+      float v = g32[i];
+      s += v * v;
+    }
+    for (int64_t i = a / 4 + threadIdx.x; i < b / 4; i += blockDim.x) {
+      const f32x4 v = ((const f32x4*)g32)[i];
+      s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+    }
+    for (int64_t i = b + threadIdx.x; i < c.end; i += blockDim.x) {
       float v = g32[i];
       s += v * v;
     }
