@@ -420,6 +420,10 @@ class MapleEngine:
         self._build_io()
         self.side = torch.cuda.Stream(device=self.device)
         self.overlap_towers = True  # False: both towers on the current stream (isolated kernel timing)
+        # enqueue (and capture) order of the two towers after the fork: the vision tower (the step's critical
+        # path) first, so its launches are dispatched ahead of the text tower's (MAPFED_TOWER_ORDER=text: the
+        # text tower first, the A/B baseline)
+        self.vision_first = os.environ.get("MAPFED_TOWER_ORDER", "vision") != "text"
         self.step_count = 0
         self.momentum_initialised = False
 
@@ -731,9 +735,13 @@ class MapleEngine:
         side = self.side if (self.overlap_towers and not reuse_text) else main
         if not reuse_text:
             side.wait_stream(main)
+        if self.vision_first:
+            self._vision_forward()
+        if not reuse_text:
             with torch.cuda.stream(side):
                 self._text_forward()
-        self._vision_forward()
+        if not self.vision_first:
+            self._vision_forward()
         if not reuse_text:
             main.wait_stream(side)
         ops.clip_head_fwd(self.img_feat, self.txt_feat, self.P["logit_scale"], self.img_n, self.txt_n, self.norms,
@@ -811,9 +819,12 @@ class MapleEngine:
         main = torch.cuda.current_stream(self.device)
         side = self.side if self.overlap_towers else main
         side.wait_stream(main)
+        if self.vision_first:
+            self._vision_backward()
         with torch.cuda.stream(side):
             self._text_backward()
-        self._vision_backward()
+        if not self.vision_first:
+            self._vision_backward()
         main.wait_stream(side)
         self._prompt_learner_bwd()
 
