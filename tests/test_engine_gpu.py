@@ -236,6 +236,33 @@ def test_eot_truncated_text_tower_matches_full(dev):
     assert worst <= 1e-2
 
 
+def test_tower_order_does_not_change_results(dev, monkeypatch):
+    """The towers' enqueue order after each fork (MAPFED_TOWER_ORDER: vision first by default, text first as
+    the A/B baseline) only changes which stream's launches reach the GPU first: every reduction is
+    deterministic, so logits, loss and every gradient are bit-identical, eagerly and in a replayed graph."""
+    J, K, B, seed = 3, 10, 4, 6
+    names = syn.synthetic_classnames(K, seed)
+    b = syn.client_batch(seed, 0, 0, B, K)
+    out = []
+    for order in ("vision", "text"):
+        monkeypatch.setenv("MAPFED_TOWER_ORDER", order)
+        e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed), device=dev)
+        assert e.vision_first == (order == "vision")
+        e.set_lr(0.0026)
+        e.load_batch(torch.from_numpy(b.images), torch.from_numpy(b.labels))
+        logits = e.forward().clone()
+        e.train_step()  # eager step (creates the momentum buffers)
+        g = e.capture_train_step()
+        g.replay()
+        torch.cuda.synchronize()
+        out.append((logits, e.loss(), {k: v.detach().clone() for k, v in e.grads().items()},
+                    e.flat16.detach().clone(), e.flat32.detach().clone()))
+    (l0, s0, g0, a0, b0), (l1, s1, g1, a1, b1) = out
+    assert torch.equal(l0, l1) and s0 == s1
+    assert all(torch.equal(g0[n], g1[n]) for n in g0)
+    assert torch.equal(a0, a1) and torch.equal(b0, b1)
+
+
 def test_c4_full_size_properties(dev):
     """BASELINE configs[3] size (B=32, K=38, J=9), where the oracle is too slow to run: size-independent
     properties.  Two engines from one seed agree bit for bit (logits, loss, every gradient, the updated
