@@ -31,6 +31,27 @@ def small_cfg(out, clients=2, rounds=1, epochs=2, extra=()):
     return cfg
 
 
+def test_c3_four_client_round(dev, tmp_path):
+    """BASELINE configs[2] (C3: 4 federated clients, EuroSAT-shape 10 classes, J = 9, batch 4) with the four
+    clients in one process: a local epoch each, then FedAvg equal to the reference's safe_average_weights (the
+    oracle) on the 4 clients' trainables, bit for bit, and every client holding the same global weights.
+    The one-client-per-GPU RCCL exchange of the same buckets is covered by tests/test_fedavg_rccl_gpu.py and
+    the gloo tests (tests/test_fedavg_dist.py)."""
+    cfg = small_cfg(tmp_path, clients=4, epochs=1, extra=["TRAINER.MAPLE.PROMPT_DEPTH", 9])
+    tr = build_trainer(cfg)
+    assert len(tr.clients) == 4 and tr.clients[0].engine.K == 10 and tr.clients[0].engine.J == 9
+    for c in tr.clients:
+        c.run_epoch(0)
+    names = tr.clients[0].engine.trainable_names
+    snaps = [{n: c.engine.P[n].detach().clone().cpu() for n in names} for c in tr.clients]
+    assert not all(torch.equal(snaps[0][n], snaps[i][n]) for n in names for i in range(1, 4))  # clients differ
+    assert tr._fedavg([]) == 4
+    ref = O.safe_average_weights(snaps)
+    for n in names:
+        for c in tr.clients:
+            assert torch.equal(c.engine.P[n].detach().cpu().float(), ref[n].float()), n
+
+
 def test_federated_round_checkpoint_and_eval_only(dev, tmp_path):
     cfg = small_cfg(tmp_path)
     tr = build_trainer(cfg)
