@@ -29,8 +29,17 @@ __global__ void im2col_kernel(const TIn* __restrict__ img, f16* __restrict__ out
   const int c = k / (P * P), kh = (k / P) % P, kw = k % P;
   const TIn* src = img + (((int64_t)b * 3 + c) * R + (py * P + kh)) * R + px * P + kw;
   f16x8 v;
+  if constexpr (sizeof(TIn) == 4) {
+    // 8 consecutive fp32 pixels: two 16-byte loads (R % 8 == 0 and P % 8 == 0 keep src 32-byte aligned)
+    const f32x4 a = *(const f32x4*)src, d = *(const f32x4*)(src + 4);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = (f16)src[e];
+    for (int e = 0; e < 4; ++e) {
+      v[e] = (f16)a[e];
+      v[4 + e] = (f16)d[e];
+    }
+  } else {
+    v = *(const f16x8*)src;
+  }
   *(f16x8*)(out + prow * K + k) = v;
 }
 
@@ -481,6 +490,7 @@ inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b
 extern "C" int mf_im2col_patch(const void* img, int img_is_f32, void* out, int B, int R, int P, void* stream) {
   if (B <= 0) return 0;
   if (R % P || (3 * P * P) % 8 || P % 8) return mf_set_error("mf_im2col_patch: bad geometry", -1);
+  if ((uintptr_t)img % 16 || (uintptr_t)out % 16) return mf_set_error("mf_im2col_patch: 16-byte aligned buffers required", -1);
   const int G = R / P;
   const int64_t total = (int64_t)B * G * G * (3 * P * P / 8);
   hipStream_t st = (hipStream_t)stream;
