@@ -433,15 +433,15 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_dkv_kernel(const f16* __restr
                                                           f16* __restrict__ dqkv, int64_t ld_dqkv, int L, int H) {
   __shared__ __attribute__((aligned(16))) f16 sQ[LQP * 64];
   __shared__ __attribute__((aligned(16))) f16 sdO[LQP * 64];
-  __shared__ float sL[LQP];
-  __shared__ float sD[LQP];
+  __shared__ __attribute__((aligned(16))) float sL[LQP];
+  __shared__ __attribute__((aligned(16))) float sD[LQP];
   const int D = H * 64;
   const int nh = blockIdx.x, n = nh / H, h = nh % H;
   const f16* base = qkv + (int64_t)n * L * ld_qkv;
   stage_rows<LQP>(sQ, base, ld_qkv, L, h * 64);
   stage_rows<LQP>(sdO, dout + (int64_t)n * L * ld_dout, ld_dout, L, h * 64);
   for (int i = threadIdx.x; i < LQP; i += blockDim.x) {
-    sL[i] = i < L ? lse[(int64_t)nh * ld_lse + i] : INFINITY;
+    sL[i] = i < L ? lse[(int64_t)nh * ld_lse + i] * 1.4426950408889634f : INFINITY;  // base 2; +inf masks
     sD[i] = i < L ? dq_dot[(int64_t)nh * ld_lse + i] : 0.f;
   }
   stage_wait();
@@ -477,12 +477,16 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_dkv_kernel(const f16* __restr
         sacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(qfr, kf[s], sacc, 0, 0, 0);
         pacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ofr, vf[s], pacc, 0, 0, 0);
       }
+      // the lane's 4 queries are consecutive: one 16-byte LDS read each for LSE and D
+      const f32x4 l4 = *(const f32x4*)(sL + qt * 16 + 4 * fg);
+      const f32x4 d4 = *(const f32x4*)(sD + qt * 16 + 4 * fg);
+      constexpr float kScaleLog2e = 0.125f * 1.4426950408889634f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int qq = qt * 16 + 4 * fg + i;
-        const bool valid = key < L && qq < L && !(CAUSAL && key > qq);
-        const float p = valid ? __expf(sacc[i] * kScale - sL[qq]) : 0.f;
-        const float ds = p * (pacc[i] - sD[qq]);
+        const bool valid = key < L && !(CAUSAL && key > qq);  // qq >= L: LSE = +inf -> p = 0
+        const float p = valid ? __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[i], kScaleLog2e, -l4[i])) : 0.f;
+        const float ds = p * (pacc[i] - d4[i]);
         pf[a * 4 + i] = (f16)p;
         dsf[a * 4 + i] = (f16)ds;
       }
@@ -541,7 +545,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_dq_kernel(const f16* __restri
     qf[s] = *(const f16x8*)(base + (int64_t)qc * ld_qkv + h * 64 + 32 * s + 8 * fg);
     of[s] = *(const f16x8*)(dout + ((int64_t)n * L + qc) * ld_dout + h * 64 + 32 * s + 8 * fg);
   }
-  const float lq = lse[(int64_t)nh * ld_lse + qc];
+  const float lq = lse[(int64_t)nh * ld_lse + qc] * 1.4426950408889634f;  // base 2
   const float dq_d = dq_dot[(int64_t)nh * ld_lse + qc];
   f32x4 dq[4];
 #pragma unroll
@@ -565,7 +569,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_dq_kernel(const f16* __restri
       for (int i = 0; i < 4; ++i) {
         const int key = kt * 16 + 4 * fg + i;
         const bool valid = key < L && q < L && !(CAUSAL && key > q);
-        const float p = valid ? __expf(sacc[i] * kScale - lq) : 0.f;
+        const float p = valid ? __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[i], 0.125f * 1.4426950408889634f, -lq)) : 0.f;
         dsf[a * 4 + i] = (f16)(p * (pacc[i] - dq_d));
       }
     }
