@@ -41,9 +41,13 @@ def draw_caption_weights(gen: torch.Generator, text_width: int = 512,
     return w.half(), W.half(), b.half()
 
 
-def caption_tokens(captions: List[str], context_length: int = syn.CONTEXT_LENGTH) -> np.ndarray:
-    """clip.tokenize(caption) (trainers/maple.py:309-311) with the build's tokenizer."""
-    return syn.tokenize(list(captions), context_length)
+def caption_tokens(captions: List[str], context_length: int = syn.CONTEXT_LENGTH, tokenizer=None) -> np.ndarray:
+    """clip.tokenize(caption) (trainers/maple.py:309-311): int64 [B, context_length] with the given tokenizer
+    (tokenizer.get_tokenizer: CLIP's BPE, or the synthetic stand-in when None); a caption longer than the
+    context raises RuntimeError as clip.tokenize does (no truncation)."""
+    from .tokenizer import get_tokenizer
+    tok = tokenizer if tokenizer is not None else get_tokenizer("")
+    return tok.tokenize(list(captions), context_length)
 
 
 def has_captions(caption) -> bool:

@@ -163,8 +163,10 @@ def get_cfg_default() -> CfgNode:
                                 TEST=CfgNode(dict(SAMPLER="SequentialSampler", BATCH_SIZE=32))))
     C.MODEL = CfgNode(dict(INIT_WEIGHTS="", NUM_CLASSES=0,
                            # PATH (MI355X addition): the local CLIP checkpoint clip._download would fetch for
-                           # NAME (trainers/maple.py:21-40); empty -> clip's download cache, else synthetic
-                           BACKBONE=CfgNode(dict(NAME="", PRETRAINED=True, PATH="")),
+                           # NAME (trainers/maple.py:21-40); empty -> clip's download cache, else synthetic.
+                           # BPE_PATH (MI355X addition): CLIP's bpe_simple_vocab_16e6.txt.gz; empty -> looked
+                           # up beside the checkpoint / in ~/.cache/clip (tokenizer.resolve_bpe_path)
+                           BACKBONE=CfgNode(dict(NAME="", PRETRAINED=True, PATH="", BPE_PATH="")),
                            HEAD=CfgNode(dict(NAME="", HIDDEN_LAYERS=(), ACTIVATION="relu", BN=True, DROPOUT=0.0))))
     C.OPTIM = CfgNode(dict(NAME="adam", LR=0.0003, WEIGHT_DECAY=5e-4, MOMENTUM=0.9, SGD_DAMPNING=0,
                            SGD_NESTEROV=False, RMSPROP_ALPHA=0.99, ADAM_BETA1=0.9, ADAM_BETA2=0.999,

@@ -31,6 +31,7 @@ import torch
 
 from . import ops
 from . import synthetic as syn
+from .tokenizer import get_tokenizer
 
 F16, F32 = torch.float16, torch.float32
 N_CTX = 2
@@ -58,6 +59,26 @@ class EngineConfig:
     # prompted blocks each append the batch's B projected caption rows, so block i runs 199 + i*B rows.
     # Buffers are sized for it at construction; a batch then needs set_captions().
     captions: bool = False
+    # CLIP's BPE merges file (bpe_simple_vocab_16e6.txt.gz) for the prompt / caption token ids
+    # (tokenizer.py); "" -> the seeded synthetic word-id tokenizer
+    bpe_path: str = ""
+
+
+def prompt_prefix(cfg: EngineConfig) -> Tuple[str, Optional[np.ndarray]]:
+    """MultiModalPromptLearner.__init__'s context (trainers/maple.py:96-106): with CTX_INIT and n_ctx <= 4 the
+    prefix is CTX_INIT ("_" -> " ") and ctx starts from the token embedding of its first n_ctx tokens (ids
+    returned); otherwise the prefix is "X X .." and ctx is drawn N(0, 0.02) (ids None)."""
+    if cfg.ctx_init and cfg.n_ctx <= 4:
+        init = cfg.ctx_init.replace("_", " ")
+        ids = get_tokenizer(cfg.bpe_path).tokenize(init, cfg.dims.context_length)[0, 1:1 + cfg.n_ctx]
+        return init, ids
+    return " ".join(["X"] * cfg.n_ctx), None
+
+
+def class_prompts(cfg: EngineConfig) -> List[str]:
+    """trainers/maple.py:136-138: prefix + " " + classname ("_" -> " ") + "."."""
+    prefix, _ = prompt_prefix(cfg)
+    return [prefix + " " + c.replace("_", " ") + "." for c in cfg.classnames]
 
 
 def _is_trainable(name: str) -> bool:
@@ -177,10 +198,15 @@ def engine_state_from_clip(clip_sd: Dict[str, np.ndarray], cfg: EngineConfig,
         elif k in ("positional_embedding", "ln_final.weight", "ln_final.bias", "text_projection") or \
                 k.startswith("transformer."):
             out["text_encoder." + k] = v
-    init = syn.tokenize(cfg.ctx_init)[0, 1:1 + cfg.n_ctx]
-    if "token_embedding.weight" in clip_sd:
-        out["prompt_learner.ctx"] = np.asarray(clip_sd["token_embedding.weight"], dtype=np.float32)[init]
+    _, init = prompt_prefix(cfg)
+    if init is None:  # no CTX_INIT: nn.init.normal_(ctx, std=0.02) (trainers/maple.py:104-105)
+        out["prompt_learner.ctx"] = syn.randn16(cfg.seed, "pl.ctx", (cfg.n_ctx, cfg.dims.text_width), 0.02)
+    elif "token_embedding.weight" in clip_sd:
+        table = np.asarray(clip_sd["token_embedding.weight"], dtype=np.float32)
+        _check_ids(init, table.shape[0])
+        out["prompt_learner.ctx"] = table[init]
     else:
+        _check_ids(init, cfg.dims.vocab_size)
         out["prompt_learner.ctx"] = syn.token_embedding_rows(cfg.seed, init)
     pl = prompt_learner if prompt_learner is not None else syn.prompt_learner_params(cfg.seed, cfg.prompt_depth,
                                                                                      cfg.n_ctx)
@@ -194,6 +220,14 @@ def engine_state_from_clip(clip_sd: Dict[str, np.ndarray], cfg: EngineConfig,
     if "token_embedding.weight" in clip_sd:
         out["clip_model2.token_embedding.weight"] = np.asarray(clip_sd["token_embedding.weight"], dtype=np.float32)
     return out
+
+
+def _check_ids(ids: np.ndarray, vocab: int):
+    """Token ids index CLIP's [vocab, 512] embedding table (on the host here, on the device for captions)."""
+    ids = np.asarray(ids)
+    if ids.size and (int(ids.min()) < 0 or int(ids.max()) >= vocab):
+        raise ValueError(f"token ids in [{int(ids.min())}, {int(ids.max())}] outside the {vocab}-row token embedding "
+                         "(a BPE merges file larger than the checkpoint's vocabulary?)")
 
 
 class _Tower:
@@ -375,6 +409,7 @@ class MapleEngine:
         size, same model), as trainers/maple.py:660-681 evaluates the model being trained."""
         self.cfg = cfg
         self.device = torch.device(device)
+        self.tokenizer = get_tokenizer(cfg.bpe_path)  # prompts and captions (CLIP BPE or the synthetic ids)
         d = cfg.dims
         self.B, self.K, self.J = cfg.batch, len(cfg.classnames), cfg.prompt_depth
         assert 1 <= self.J <= 12, "PROMPT_DEPTH must be in [1, 12]"
@@ -506,12 +541,14 @@ class MapleEngine:
         """token prefix / suffix buffers and the EOT gather index (trainers/maple.py:136-149)."""
         cfg = self.cfg
         d = cfg.dims
-        texts = [f"{cfg.ctx_init} {c.replace('_', ' ')}." for c in cfg.classnames]
-        tok = syn.tokenize(texts, d.context_length)
+        texts = class_prompts(cfg)
+        tok = self.tokenizer.tokenize(texts, d.context_length)
         self.tokenized = torch.from_numpy(tok)
         if self._token_table is not None:  # the checkpoint's token embedding (trainers/maple.py:140-143)
+            _check_ids(tok, self._token_table.shape[0])
             emb = self._token_table.cpu()[torch.from_numpy(tok.reshape(-1))].numpy()
         else:
+            _check_ids(tok, d.vocab_size)
             emb = syn.token_embedding_rows(cfg.seed, tok.reshape(-1), d.text_width)
         emb = emb.reshape(len(texts), d.context_length, d.text_width)
         dev = self.device
@@ -631,6 +668,9 @@ class MapleEngine:
         tok = torch.as_tensor(tokens)
         if tuple(tok.shape) != tuple(self.cap_tokens.shape):
             raise ValueError(f"caption tokens {tuple(tok.shape)}; expected {tuple(self.cap_tokens.shape)}")
+        # mf_caption_pool gathers table rows by id on the device: range-check on the host first (token tensors
+        # passed directly, trainers/maple.py:310-311, bypass the tokenizer)
+        _check_ids(tok.cpu().numpy(), self.cfg.dims.vocab_size)
         self.cap_tokens.copy_(tok.to(torch.int32), non_blocking=True)
         w, W, b = weights
         self.cap_w.copy_(w, non_blocking=True)

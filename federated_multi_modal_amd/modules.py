@@ -312,6 +312,10 @@ class CustomCLIP(nn.Module):
         self.clip_model2 = c
         self._by_name = {n: cache[id(engine.P[n])] for n in engine.trainable_names}
         self._eval: Dict[object, MapleEngine] = {}
+        # where the caption path's random AttentionPooling / Linear weights come from: torch's global CPU
+        # generator, as in the reference (clip/model.py:461, 557); the federated trainer assigns each client
+        # its own seeded generator here, and its training step draws from the same attribute
+        self.caption_generator: torch.Generator = torch.default_generator
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         """nn.Module.load_state_dict semantics on the engine (MapleEngine.load_state_dict: strict key check
@@ -338,8 +342,9 @@ class CustomCLIP(nn.Module):
     def _caption_engine(self, batch: int, caption) -> MapleEngine:
         """The caption path (trainers/maple.py:307-322 -> clip/model.py:550-561) for a batch: an engine with
         the growing vision sequence (shared parameters), this batch's caption tokens, and the random
-        AttentionPooling vector / Linear(512, 768) drawn from torch's global CPU generator, as the reference
-        draws them in every such forward (captions.draw_caption_weights reproduces its draws)."""
+        AttentionPooling vector / Linear(512, 768) drawn from self.caption_generator (torch's global CPU
+        generator unless the trainer set a per-client one), as the reference draws them in every such forward
+        (captions.draw_caption_weights reproduces its draws)."""
         e = self.engine[0]
         key = ("captions", batch)
         if key not in self._eval:
@@ -347,10 +352,10 @@ class CustomCLIP(nn.Module):
                                           shared=e)
         ce = self._eval[key]
         if all(isinstance(c, str) for c in caption):
-            tok = caption_tokens(list(caption), ce.cfg.dims.context_length)
+            tok = caption_tokens(list(caption), ce.cfg.dims.context_length, ce.tokenizer)
         else:
             tok = torch.stack([torch.as_tensor(c) for c in caption]).cpu()
-        ce.set_captions(tok, draw_caption_weights(torch.default_generator))
+        ce.set_captions(tok, draw_caption_weights(self.caption_generator))
         return ce
 
     def forward(self, image, label=None, caption=None, return_feature=False):

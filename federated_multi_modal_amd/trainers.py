@@ -10,9 +10,10 @@ What runs where:
     hipGraph per step; the loss, NaN flags and accuracy counters stay on the device and are read
     once per epoch instead of ~150 host syncs per step (trainers/maple.py:601-615);
   * the LR schedule is Dassl's, evaluated on the host (schedule.py) and handed to the SGD kernel;
-  * FedAvg is FedAvgBucket: one client per rank with an RCCL all-reduce when launched with
-    torch.distributed (WORLD_SIZE == FED.NUM_CLIENTS), or the reference's sequential clients in one
-    process (their buckets summed in client order).
+  * FedAvg is FedAvgExchange over the clients' FedAvgBuckets: launched with torch.distributed, the
+    FED.NUM_CLIENTS clients are split over the ranks in contiguous blocks (one client per GPU when
+    WORLD_SIZE == FED.NUM_CLIENTS, several trained one after another per rank otherwise) and exchanged
+    over RCCL; launched as one process, the reference's sequential clients (buckets summed in client order).
 
 Error behaviour kept: NaN/Inf loss -> RuntimeError("NaN/Inf in total loss") from run_epoch
 (caught per client by the round loop, trainers/maple_fed.py:262-265); non-finite inputs ->
@@ -31,10 +32,11 @@ import torch.distributed as dist
 from . import ops
 from .data import DATASET_CLASSES, SyntheticClientDataManager, unified_classnames
 from .engine import EngineConfig, MapleEngine
-from .federated import FedAvgBucket, reduce_local
+from .federated import FedAvgBucket, FedAvgExchange, FederatedAbort
 from .captions import caption_tokens, draw_caption_weights, has_captions
 from .modules import CustomCLIP
 from .schedule import HostLR
+from .tokenizer import BPE_FILE, describe as describe_tokenizer, get_tokenizer, resolve_bpe_path
 
 
 class Registry:
@@ -72,6 +74,8 @@ def _device(cfg) -> torch.device:
     if not torch.cuda.is_available():
         raise RuntimeError("the MI355X trainers need a GPU (libmapfed.so kernels); none is visible")
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("MAPFED_DIST_BACKEND", "nccl") != "nccl":
+        local %= torch.cuda.device_count()  # the gloo rehearsal: several ranks share the box's GPU(s)
     return torch.device("cuda", local)
 
 
@@ -160,12 +164,20 @@ class MaPLe(TrainerX):
         classnames = self.classnames
         state, dims = None, None
         backbone = _backbone_file(cfg)
+        bpe = resolve_bpe_path(cfg.MODEL.BACKBONE.get("BPE_PATH", "") if hasattr(cfg.MODEL.BACKBONE, "get") else "",
+                               backbone)
+        tok = get_tokenizer(bpe)
+        if self.client_id in (None, 0):
+            print(f"[INFO] tokenizer: {describe_tokenizer(tok)}")
+            if backbone and tok.kind != "bpe":
+                print(f"[WARN] CLIP checkpoint {backbone} with the synthetic tokenizer: put {BPE_FILE} beside it "
+                      "or set MODEL.BACKBONE.BPE_PATH, or the prompts do not match CLIP's")
         if backbone:
-            state, dims = _load_clip_weights(backbone, cfg, classnames, mcfg)
+            state, dims = _load_clip_weights(backbone, cfg, classnames, mcfg, bpe)
         ecfg = EngineConfig(batch=cfg.DATALOADER.TRAIN_X.BATCH_SIZE, classnames=list(classnames),
                             prompt_depth=mcfg.PROMPT_DEPTH, seed=max(cfg.SEED, 0), n_ctx=mcfg.N_CTX,
                             ctx_init=mcfg.CTX_INIT, momentum=cfg.OPTIM.MOMENTUM,
-                            weight_decay=cfg.OPTIM.WEIGHT_DECAY)
+                            weight_decay=cfg.OPTIM.WEIGHT_DECAY, bpe_path=bpe)
         if dims is not None:
             ecfg.dims = dims
         if cfg.OPTIM.NAME != "sgd":
@@ -182,8 +194,9 @@ class MaPLe(TrainerX):
         self._graphs = {}
         self._cap_engine: Optional[MapleEngine] = None
         # the caption path's random AttentionPooling / Linear draws (captions.py): a per-client generator in
-        # place of the reference's global one
+        # place of the reference's global one, shared by the training step and model(image, label, caption)
         self._cap_gen = torch.Generator().manual_seed(max(cfg.SEED, 0) * 1000 + (self.client_id or 0))
+        self.model.caption_generator = self._cap_gen
         self._loss_sum = torch.zeros(1, device=self.device)
         self._bad = torch.zeros(1, device=self.device)
         self._ok = torch.zeros(1, device=self.device)   # steps of the epoch before its first non-finite loss
@@ -218,10 +231,10 @@ class MaPLe(TrainerX):
                                            shared=self.engine)
         ce = self._cap_engine
         if all(isinstance(c, str) for c in caption):
-            tok = caption_tokens(caption, ce.cfg.dims.context_length)
+            tok = caption_tokens(caption, ce.cfg.dims.context_length, ce.tokenizer)
         else:
             tok = torch.stack([torch.as_tensor(c) for c in caption]).cpu()
-        ce.set_captions(tok, draw_caption_weights(self._cap_gen))
+        ce.set_captions(tok, draw_caption_weights(self.model.caption_generator))
         return ce
 
     def _load(self, image, label, e=None):
@@ -419,22 +432,19 @@ def load_pretrained_weights(model, weight_path):
         print(f"** The following layers are discarded due to unmatched keys or layer size: {discarded[:10]}")
 
 
-def _load_clip_weights(path, cfg, classnames, mcfg):
-    """A CLIP checkpoint: a state dict saved with torch.save (loaded with weights_only=True: no code
-    runs), or the TorchScript archive clip._download fetches (its parameters are read through
-    torch.jit.load, as load_clip_to_cpu does first, trainers/maple.py:27-31)."""
+def _load_clip_weights(path, cfg, classnames, mcfg, bpe_path=""):
+    """A CLIP checkpoint (load_clip_to_cpu, trainers/maple.py:21-40): the TorchScript archive clip._download
+    fetches, or a state dict saved with torch.save -- read by clip_archive.load_clip_state_dict, which
+    executes nothing from the file (an allow-listed unpickler over the archive's tensors, or torch.load
+    with weights_only=True)."""
+    from .clip_archive import load_clip_state_dict
     from .engine import check_dims, clip_dims_from_state_dict, engine_state_from_clip
-    try:
-        sd = torch.load(path, map_location="cpu", weights_only=True)
-    except Exception:  # the official archives are TorchScript (zip with code/), not a plain state dict
-        sd = torch.jit.load(path, map_location="cpu").state_dict()
-    if isinstance(sd, dict) and "state_dict" in sd:
-        sd = sd["state_dict"]
+    sd = load_clip_state_dict(path)
     sd = {k: v.float().numpy() for k, v in sd.items() if k not in ("input_resolution", "context_length", "vocab_size")}
     dims = clip_dims_from_state_dict(sd)  # clip/model.py:750-777
     check_dims(dims)
     ecfg = EngineConfig(batch=1, classnames=list(classnames), prompt_depth=mcfg.PROMPT_DEPTH, seed=max(cfg.SEED, 0),
-                        n_ctx=mcfg.N_CTX, ctx_init=mcfg.CTX_INIT, dims=dims)
+                        n_ctx=mcfg.N_CTX, ctx_init=mcfg.CTX_INIT, dims=dims, bpe_path=bpe_path)
     return engine_state_from_clip(sd, ecfg), dims
 
 
@@ -442,9 +452,10 @@ def _load_clip_weights(path, cfg, classnames, mcfg):
 class MaPLeFederated(TrainerX):
     """The federated aggregator (trainers/maple_fed.py:24-500).
 
-    Process layout: launched with torch.distributed (WORLD_SIZE == FED.NUM_CLIENTS, backend nccl =
-    RCCL), rank r trains client r on its own GPU and FedAvg is an all-reduce; launched as one
-    process, the clients train one after another on one GPU, as in the reference."""
+    Process layout: launched with torch.distributed (backend nccl = RCCL), FED.NUM_CLIENTS must be a
+    multiple of WORLD_SIZE: rank r trains clients r*C .. r*C + C - 1 (C = NUM_CLIENTS / WORLD_SIZE) one
+    after another on its GPU, as the reference trains all of them on one (trainers/maple_fed.py:247), and
+    FedAvg exchanges every rank's C buckets; launched as one process, every client trains on one GPU."""
 
     CLIENT_DATASETS = ("PatternNet", "Ucmerced", "EuroSAT")
 
@@ -459,13 +470,18 @@ class MaPLeFederated(TrainerX):
         self.nan_stats = {"total_updates": 0, "failed_clients": [], "skipped_rounds": 0}
         self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         self.rank = dist.get_rank() if self.distributed else 0
-        if self.distributed and dist.get_world_size() != self.num_clients:
-            raise ValueError(f"WORLD_SIZE {dist.get_world_size()} != FED.NUM_CLIENTS {self.num_clients}: "
-                             "one client per rank")
+        if self.distributed and self.num_clients % dist.get_world_size():
+            raise ValueError(f"FED.NUM_CLIENTS {self.num_clients} is not a multiple of WORLD_SIZE "
+                             f"{dist.get_world_size()}: each rank trains the same number of clients")
         super().__init__(cfg)
 
     def _local_client_ids(self) -> List[int]:
-        return [self.rank] if self.distributed else list(range(self.num_clients))
+        """This process's clients: a contiguous block, so [rank][local index] is the global client order the
+        ordered FedAvg sums in."""
+        if not self.distributed:
+            return list(range(self.num_clients))
+        per = self.num_clients // dist.get_world_size()
+        return list(range(self.rank * per, (self.rank + 1) * per))
 
     def _disk_datasets(self) -> bool:
         root = self.cfg.DATASET.ROOT
@@ -521,30 +537,40 @@ class MaPLeFederated(TrainerX):
         self.register_model("MultiModalPromptLearner_Aggregator", c0.model, None, None)
         mode = self.cfg.FED.get("AGGREGATION", "ordered") if hasattr(self.cfg.FED, "get") else "ordered"
         self.fed = [FedAvgBucket(c.engine, mode=mode) for c in self.clients]
+        self.exchange = FedAvgExchange(self.fed, mode=mode)
         self.global_weights = self.clients[0].model.state_dict()
 
     # ---------------------------------------------------------------- round loop
     def train(self):
         """trainers/maple_fed.py:228-303.
 
-        FedAvg overlap: a client's bucket is packed and its exchange (RCCL all_gather or all_reduce,
-        federated.py) launched right after its last local epoch's SGD steps and LR update, before that
-        epoch's test() (trainers/maple.py:646), which only reads the weights; the collective flies while
-        the test batches run and is waited for after the client loop.  The result equals the reference's
-        FedAvg-after-training order: the test reads the same local weights and the bucket holds them."""
+        FedAvg overlap: each client's bucket is packed right after its last local epoch's SGD steps and LR
+        update, before that epoch's test() (trainers/maple.py:646), which only reads the weights; after the
+        rank's last client packs, the exchange (federated.FedAvgExchange) is launched there, flies while the
+        test batches run, and is waited for after the client loop.  The result equals the reference's
+        FedAvg-after-training order: the test reads the same local weights and the bucket holds them.  A
+        client whose test() then raises is still excluded (finish re-exchanges with its vote withdrawn)."""
         for round_idx in range(self.num_rounds):
             print(f"\n--- Federated Round {round_idx + 1}/{self.num_rounds} ---")
             self.broadcast_weights()
-            round_losses, failed_local = [], []
-            for trainer, fed in zip(self.clients, self.fed):
+            round_losses, late_failed, abort = [], [], None
+            n_local = len(self.clients)
+            for j, (trainer, fed) in enumerate(zip(self.clients, self.fed)):
+                if abort is not None:  # this rank is stopping: its remaining clients only vote "failed"
+                    fed.pack(failed=True)
+                    if j == n_local - 1:
+                        self.exchange.start()
+                    continue
                 print(f"[Client {trainer.client_id}] local training ...")
                 trainer.epoch = round_idx * self.local_epochs
                 trainer.max_epoch = (round_idx + 1) * self.local_epochs
                 last = 0.0
-                started = []
+                started, failed = [], False
 
-                def start_fedavg(fed=fed, started=started):
-                    fed.start(collective=self.distributed)
+                def start_fedavg(fed=fed, started=started, last_local=j == n_local - 1):
+                    fed.pack()
+                    if last_local:
+                        self.exchange.start()
                     started.append(True)
                 try:
                     for ep in range(trainer.epoch, trainer.max_epoch):
@@ -554,12 +580,27 @@ class MaPLeFederated(TrainerX):
                 except RuntimeError as err:
                     print(f"Client {trainer.client_id} failed training: {err}")
                     self.nan_stats["failed_clients"].append(trainer.client_id)
-                    failed_local.append(trainer.client_id)
+                    failed = True
+                    if started:  # failed in its last test(), after its bucket went out
+                        late_failed.append(j)
+                except Exception as err:  # not caught by the reference (its process dies): with peers, make
+                    if not self.distributed:  # every rank stop at this round's exchange instead of hanging
+                        raise
+                    abort, failed = err, True
+                    if started:
+                        late_failed.append(j)
                 if not started:  # failed, or no local epochs: pack (excluded when failed) and exchange now
-                    fed.start(collective=self.distributed, failed=trainer.client_id in failed_local)
+                    fed.pack(failed=failed)
+                    if j == n_local - 1:
+                        self.exchange.start()
             if round_losses:
                 print(f"[Round {round_idx + 1}] Avg local training loss = {sum(round_losses) / len(round_losses):.4f}")
-            n_valid = self._fedavg_finish()
+            try:
+                n_valid = self._fedavg_finish(late_failed, abort=abort is not None)
+            except FederatedAbort:
+                if abort is not None:
+                    raise abort
+                raise
             if n_valid > 0:
                 self.nan_stats["total_updates"] += 1
             else:
@@ -575,15 +616,16 @@ class MaPLeFederated(TrainerX):
         """check_weights_valid + safe_average_weights + broadcast, on the device (federated.py), for
         clients that finished training: pack every local client, exchange, unpack."""
         for c, fed in zip(self.clients, self.fed):
-            fed.start(collective=self.distributed, failed=c.client_id in failed_local)
-        return self._fedavg_finish()
+            fed.pack(failed=c.client_id in failed_local)
+        self.exchange.start()
+        return self._fedavg_finish([])
 
-    def _fedavg_finish(self) -> int:
-        """Wait for the exchange every local client started (FedAvgBucket.start), reduce, unpack."""
-        if not self.distributed:
-            reduce_local(self.fed)  # sequential clients in one process: their buckets summed in client order
+    def _fedavg_finish(self, late_failed=(), abort: bool = False) -> int:
+        """Wait for the exchange the rank's last client started (FedAvgExchange: every client's bucket then
+        holds the sum over all clients), unpack into every local client."""
+        self.exchange.finish(late_failed, abort=abort)
         for fed in self.fed:
-            fed.finish()
+            fed.unpack()
         return self.fed[0].n_valid()
 
     # ---------------------------------------------------------------- reference utilities

@@ -34,11 +34,21 @@ def load_case(name: str) -> Dict[str, np.ndarray]:
 
 
 def case_inputs(c: Dict[str, np.ndarray]):
-    """(J, K, B, seed, classnames, ClientBatch) of a case."""
+    """(J, K, B, seed, classnames, ClientBatch) of a case (class names stored in BPE cases, else synthetic)."""
     J, K, B, seed = int(c["J"]), int(c["K"]), int(c["B"]), int(c["seed"])
-    names = syn.synthetic_classnames(K, seed)
+    names = [str(n) for n in c["classnames"]] if "classnames" in c else syn.synthetic_classnames(K, seed)
     batch = syn.client_batch(seed, int(c["client"]), int(c["step"]), B, K)
     return J, K, B, seed, names, batch
+
+
+def case_bpe_path(c: Dict[str, np.ndarray]) -> str:
+    """The merges file a case was tokenized with ("" = the synthetic word ids)."""
+    return str(GOLD / str(c["bpe"])) if "bpe" in c else ""
+
+
+def case_tokenizer(c: Dict[str, np.ndarray]):
+    from federated_multi_modal_amd.tokenizer import get_tokenizer
+    return get_tokenizer(case_bpe_path(c))
 
 
 def trace_idx(case: str, key: str, n: int) -> np.ndarray:

@@ -138,6 +138,69 @@ def load_reference():
     return model, maple, maple_fed
 
 
+def load_reference_tokenizer(bpe_path: str):
+    """The reference's own tokenizer over a merges file: clip/simple_tokenizer.py (SimpleTokenizer) and
+    clip/clip.py (tokenize), loaded by file path as the package `refclip_bpe`.  Wiring only:
+      * ftfy is absent: a stub module whose fix_text returns its input (the fixtures hold only text
+        ftfy leaves unchanged; see federated_multi_modal_amd/tokenizer.py);
+      * torchvision is absent: clip.py imports its transforms at module level for `_transform`, which
+        tokenize never touches -- stub classes stand in;
+      * clip.py builds its module-level `_tokenizer = _Tokenizer()` with the default merges path (absent):
+        the default argument is pointed at `bpe_path` before clip.py is executed.
+    Returns (SimpleTokenizer instance, clip.tokenize function, the clip module)."""
+    key = ("bpe", str(bpe_path))
+    if key in _CACHE:
+        return _CACHE[key]
+    load_reference()  # the model module (clip.py does `from .model import build_model`)
+    if "ftfy" not in sys.modules:
+        ftfy = types.ModuleType("ftfy")
+        ftfy.fix_text = lambda text, *a, **k: text
+        sys.modules["ftfy"] = ftfy
+    if "torchvision" not in sys.modules:
+        tv = types.ModuleType("torchvision")
+        tr = types.ModuleType("torchvision.transforms")
+        for n in ("Compose", "Resize", "CenterCrop", "ToTensor", "Normalize"):
+            setattr(tr, n, type(n, (), {"__init__": lambda self, *a, **k: None}))
+        tr.InterpolationMode = types.SimpleNamespace(BICUBIC="bicubic")
+        tv.transforms = tr
+        sys.modules["torchvision"], sys.modules["torchvision.transforms"] = tv, tr
+    pkg_name = f"refclip_bpe{len([k for k in _CACHE if isinstance(k, tuple)])}"
+    pkg = types.ModuleType(pkg_name)
+    pkg.__path__ = []
+    sys.modules[pkg_name] = pkg
+    sys.modules[pkg_name + ".model"] = _CACHE["model"]
+    st = _load(pkg_name + ".simple_tokenizer", REF / "clip" / "simple_tokenizer.py")
+    st.SimpleTokenizer.__init__.__defaults__ = (str(bpe_path),)
+    spec = importlib.util.spec_from_file_location(pkg_name + ".clip", str(REF / "clip" / "clip.py"))
+    clip_mod = importlib.util.module_from_spec(spec)
+    clip_mod.__package__ = pkg_name
+    sys.modules[pkg_name + ".clip"] = clip_mod
+    spec.loader.exec_module(clip_mod)
+    res = (st.SimpleTokenizer(str(bpe_path)), clip_mod.tokenize, clip_mod)
+    _CACHE[key] = res
+    return res
+
+
+class reference_bpe:
+    """`with reference_bpe(path):` the reference's trainers/maple.py tokenizes with its own BPE tokenizer
+    over `path` (its module globals `clip` -> the loaded clip/clip.py, `_tokenizer` -> SimpleTokenizer)
+    instead of the synthetic stand-in the other fixtures use."""
+
+    def __init__(self, bpe_path):
+        self.bpe_path = bpe_path
+
+    def __enter__(self):
+        _, maple, _ = load_reference()
+        tok, _, clip_mod = load_reference_tokenizer(self.bpe_path)
+        self.saved = (maple.clip, maple._tokenizer)
+        maple.clip, maple._tokenizer = clip_mod, tok
+        return self
+
+    def __exit__(self, *exc):
+        _, maple, _ = load_reference()
+        maple.clip, maple._tokenizer = self.saved
+
+
 class cuda_as_cpu:
     """The reference's caption path hard-codes `.to("cuda")` (clip/model.py:461, 554, 557); on this CPU-only
     host `with cuda_as_cpu():` maps a "cuda" device argument of Tensor.to / Module.to to "cpu" for the

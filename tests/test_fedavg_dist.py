@@ -106,7 +106,7 @@ def _worker(rank, world, port, bad_ranks, mode, out):
     dist.destroy_process_group()
 
 
-def _spawn(fn, world, *args):
+def _spawn(fn, world, *args):  # noqa: D103
     port = _free_port()
     mgr = mp.Manager()
     out = mgr.dict()
@@ -139,6 +139,53 @@ def test_fedavg_exchange_matches_reference(world, bad, mode):
     assert all(torch.equal(res[0][1], res[r][1]) and torch.equal(res[0][2], res[r][2]) for r in range(world))
 
 
+def _group_worker(rank, world, port, per_rank, bad, mode, out):
+    """Several clients per rank (clients rank*C .. rank*C + C - 1) through one FedAvgExchange."""
+    _init(rank, world, port)
+    from federated_multi_modal_amd.federated import FedAvgBucket, FedAvgExchange
+    ids = list(range(rank * per_rank, (rank + 1) * per_rank))
+    engines = [FakeEngine(c, bad=c in bad) for c in ids]
+    feds = []
+    for e in engines:
+        loc16, loc32 = e.flat16.clone(), e.flat32.clone()
+        e.flat16.copy_(FakeEngine(0).flat16)
+        e.flat32.copy_(FakeEngine(0).flat32)
+        feds.append(FedAvgBucket(e, kernels=HostKernels, mode=mode))
+        e.flat16.copy_(loc16)
+        e.flat32.copy_(loc32)
+    x = FedAvgExchange(feds, mode=mode)
+    for f in feds:
+        f.pack()
+    x.start()
+    x.finish([])
+    for f in feds:
+        f.unpack()
+    out[rank] = (feds[0].n_valid(), [(e.flat16.clone(), e.flat32.clone()) for e in engines])
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,per_rank,bad,mode", [(2, 2, (), "ordered"), (3, 2, (4,), "ordered"),
+                                                     (2, 3, (), "allreduce")])
+def test_fedavg_several_clients_per_rank(world, per_rank, bad, mode):
+    """FED.NUM_CLIENTS a multiple of WORLD_SIZE: every client of every rank ends with
+    safe_average_weights over all valid clients -- bit for bit in the ordered mode (the all_to_all delivers
+    [source rank][local client] = the reference's client order)."""
+    res = _spawn(_group_worker, world, per_rank, tuple(bad), mode)
+    clients = [FakeEngine(c, bad=c in bad) for c in range(world * per_rank)]
+    valid = [c for c in clients if O.check_weights_valid({"a": c.flat16, "b": c.flat32})]
+    ref = O.safe_average_weights([{"a": c.flat16, "b": c.flat32} for c in valid])
+    for r in range(world):
+        n_valid, weights = res[r]
+        assert n_valid == len(valid)
+        for p16, p32 in weights:
+            if mode == "ordered":
+                assert torch.equal(p16, ref["a"]) and torch.equal(p32, ref["b"].float())
+            else:  # another fp32 summation order: one fp16 ulp, plus fp32 cancellation of the largest inputs
+                ulp = torch.exp2(torch.floor(torch.log2(ref["b"].float().abs().clamp_min(2.0 ** -14))) - 10)
+                big = torch.stack([c.flat32.abs() for c in valid]).max(0).values
+                assert ((p32 - ref["b"].float()).abs() <= ulp + 1e-6 * big).all()
+
+
 # ----------------------------------------------------------------------------- the round loop itself
 
 class _Optim:
@@ -155,12 +202,14 @@ class FakeClient:
     deterministic per-(client, round, epoch) update, fails with the reference's RuntimeError when told,
     calls before_test exactly where MaPLe.run_epoch does, and logs the order of events."""
 
-    def __init__(self, rank, fail_rounds=()):
+    def __init__(self, rank, fail_rounds=(), late_fail_rounds=(), abort_round=None):
         self.client_id = rank
         self.engine = FakeEngine(0)  # every client starts from the same global weights
         self.optim = _Optim()
         self.sched = None
         self.fail_rounds = set(fail_rounds)
+        self.late_fail_rounds = set(late_fail_rounds)  # test() of the last epoch raises (after FedAvg started)
+        self.abort_round = abort_round                 # a ValueError (not caught by the reference) that round
         self.events = []
         self.model = self
 
@@ -178,11 +227,16 @@ class FakeClient:
         if round_idx in self.fail_rounds and ep % 2 == 1:
             self.events.append(("fail", ep))
             raise RuntimeError("NaN/Inf in total loss")
+        if round_idx == self.abort_round:
+            self.events.append(("abort", ep))
+            raise ValueError("NaN/Inf values in input image")
         self.local_update(self.client_id, round_idx, ep, self.engine)
         if before_test is not None:
             self.events.append(("fedavg_start", ep))
             before_test()
         self.events.append(("test", ep))
+        if before_test is not None and round_idx in self.late_fail_rounds:
+            raise RuntimeError("kernel failure in test()")
         return {"avg_loss": 1.0}
 
     def test(self, evaluate_train=False):
@@ -190,40 +244,54 @@ class FakeClient:
         return {"accuracy": 50.0}
 
 
-def _train_worker(rank, world, port, fail, out):
+def _train_worker(rank, world, port, per_rank, fail, late, abort, out):
     _init(rank, world, port)
     from federated_multi_modal_amd.config import extend_cfg, get_cfg_default
-    from federated_multi_modal_amd.federated import FedAvgBucket
+    from federated_multi_modal_amd.federated import FedAvgBucket, FedAvgExchange
     from federated_multi_modal_amd.trainers import MaPLeFederated
     cfg = get_cfg_default()
     extend_cfg(cfg)
     cfg.OUTPUT_DIR = f"/tmp/mapfed_fedtest_{port}"
     tr = MaPLeFederated.__new__(MaPLeFederated)   # the round loop without building GPU engines
-    tr.cfg, tr.num_clients, tr.num_rounds, tr.local_epochs = cfg, world, 2, 2
+    tr.cfg, tr.num_clients, tr.num_rounds, tr.local_epochs = cfg, world * per_rank, 2, 2
     tr.nan_stats = {"total_updates": 0, "failed_clients": [], "skipped_rounds": 0}
     tr.distributed, tr.rank = True, rank
-    client = FakeClient(rank, fail_rounds=fail.get(rank, ()))
-    tr.clients = [client]
-    tr.fed = [FedAvgBucket(client.engine, kernels=HostKernels, mode="ordered")]
+    ids = list(range(rank * per_rank, (rank + 1) * per_rank))
+    tr.clients = [FakeClient(c, fail_rounds=fail.get(c, ()), late_fail_rounds=late.get(c, ()),
+                             abort_round=abort.get(c)) for c in ids]
+    tr.fed = [FedAvgBucket(c.engine, kernels=HostKernels, mode="ordered") for c in tr.clients]
+    tr.exchange = FedAvgExchange(tr.fed, mode="ordered")
     tr.save_model = lambda *a, **k: None
-    tr.train()
-    out[rank] = (client.engine.flat16.clone(), client.engine.flat32.clone(), list(client.events), dict(tr.nan_stats),
-                 client.engine.momentum_resets)
+    err = None
+    try:
+        tr.train()
+    except Exception as exc:  # noqa: BLE001 - the abort cases end here on every rank
+        err = f"{type(exc).__name__}: {exc}"
+    out[rank] = ([(c.engine.flat16.clone(), c.engine.flat32.clone()) for c in tr.clients],
+                 [list(c.events) for c in tr.clients], dict(tr.nan_stats),
+                 [c.engine.momentum_resets for c in tr.clients], err)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,fail", [(2, {}), (3, {1: (0,)}), (2, {0: (1,), 1: (1,)})])
-def test_round_loop_distributed(world, fail):
-    """MaPLeFederated.train() on gloo ranks: 2 rounds x 2 local epochs; each client's FedAvg exchange starts
-    inside its last local epoch, after the SGD steps and before that epoch's test() (the overlap), and the
-    global weights after every round equal safe_average_weights over the clients that did not fail,
-    bit for bit; an all-failed round keeps the previous global weights (trainers/maple_fed.py:262-303)."""
-    res = _spawn(_train_worker, world, fail)
+@pytest.mark.parametrize("world,per_rank,fail,late", [
+    (2, 1, {}, {}), (3, 1, {1: (0,)}, {}), (2, 1, {0: (1,), 1: (1,)}, {}),
+    (2, 2, {1: (0,)}, {}),                 # 4 clients on 2 ranks, trained two after another per rank
+    (2, 1, {}, {1: (1,)}), (2, 2, {}, {0: (0,), 3: (1,)}),  # a client's last test() fails after its bucket went out
+])
+def test_round_loop_distributed(world, per_rank, fail, late):
+    """MaPLeFederated.train() on gloo ranks: 2 rounds x 2 local epochs; each client's bucket is packed inside
+    its last local epoch, after the SGD steps and before that epoch's test() (the rank's last client starts
+    the exchange there: the overlap), and the global weights after every round equal safe_average_weights
+    over the clients that did not fail, bit for bit -- also for a client whose last test() raises after
+    its bucket went out; an all-failed round keeps the previous global weights
+    (trainers/maple_fed.py:247-303)."""
+    res = _spawn(_train_worker, world, per_rank, fail, late, {})
+    n = world * per_rank
     # expected: replay the rounds on the host with the reference's aggregation
     g16, g32 = FakeEngine(0).flat16.clone(), FakeEngine(0).flat32.clone()
     for r in range(2):
         locals_ = []
-        for c in range(world):
+        for c in range(n):
             e = FakeEngine(0)
             e.flat16.copy_(g16)
             e.flat32.copy_(g32)
@@ -232,24 +300,39 @@ def test_round_loop_distributed(world, fail):
                 if failed and ep % 2 == 1:
                     break
                 FakeClient.local_update(c, r, ep, e)
-            if not failed:
+            if not failed and r not in late.get(c, ()):
                 locals_.append({"a": e.flat16, "b": e.flat32})
         if locals_:
             avg = O.safe_average_weights(locals_)
             g16, g32 = avg["a"], avg["b"].float()
     for rank in range(world):
-        p16, p32, events, stats, resets = res[rank]
-        assert torch.equal(p16, g16) and torch.equal(p32, g32), rank
-        assert resets == 2  # broadcast_weights drops the SGD momentum every round
-        for r in range(2):
-            if r in fail.get(rank, ()):
-                assert ("fail", 2 * r + 1) in events
-                continue
-            i = events.index(("fedavg_start", 2 * r + 1))
-            assert events[i + 1] == ("test", 2 * r + 1)      # the exchange overlaps the last local test
-            assert ("fedavg_start", 2 * r) not in events       # started once per round, in the last epoch
-    n_failed = sum(len(v) for v in fail.values())
-    assert res[0][3]["failed_clients"].__len__() == len(fail.get(0, ()))
-    skipped = sum(1 for r in range(2) if all(r in fail.get(c, ()) for c in range(world)))
-    assert res[0][3]["skipped_rounds"] == skipped and res[0][3]["total_updates"] == 2 - skipped
-    assert n_failed >= 0
+        weights, events, stats, resets, err = res[rank]
+        assert err is None, err
+        for j, (p16, p32) in enumerate(weights):
+            c = rank * per_rank + j
+            assert torch.equal(p16, g16) and torch.equal(p32, g32), c
+            assert resets[j] == 2  # broadcast_weights drops the SGD momentum every round
+            ev = events[j]
+            for r in range(2):
+                if r in fail.get(c, ()):
+                    assert ("fail", 2 * r + 1) in ev
+                    continue
+                i = ev.index(("fedavg_start", 2 * r + 1))
+                assert ev[i + 1] == ("test", 2 * r + 1)      # the exchange overlaps the last local test
+                assert ("fedavg_start", 2 * r) not in ev       # packed once per round, in the last epoch
+        local_failed = sum(len(fail.get(c, ())) + len(late.get(c, ())) for c in range(rank * per_rank,
+                                                                                     (rank + 1) * per_rank))
+        assert len(stats["failed_clients"]) == local_failed
+    skipped = sum(1 for r in range(2) if all(r in fail.get(c, ()) or r in late.get(c, ()) for c in range(n)))
+    assert res[0][2]["skipped_rounds"] == skipped and res[0][2]["total_updates"] == 2 - skipped
+
+
+def test_round_loop_abort_stops_every_rank():
+    """A non-finite input raises ValueError on one rank (trainers/maple.py:526-535; the reference does not
+    catch it and its process dies): every rank leaves train() at that round's exchange -- the failing rank
+    with its ValueError, its peers with FederatedAbort -- instead of waiting in the next round's collectives."""
+    res = _spawn(_train_worker, 3, 1, {}, {}, {1: 1})
+    assert res[1][4].startswith("ValueError")
+    assert res[0][4].startswith("FederatedAbort") and res[2][4].startswith("FederatedAbort")
+    for rank in range(3):
+        assert res[rank][2]["total_updates"] == 1   # round 0 completed everywhere

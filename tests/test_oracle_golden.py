@@ -99,7 +99,9 @@ def test_oracle_matches_reference_case(name):
     block output of both towers (clip/model.py:307-352) too."""
     c = C.load_case(name)
     J, K, B, seed, names, batch = C.case_inputs(c)
-    M = O.build_model(seed, J, names)
+    M = O.build_model(seed, J, names, tokenizer=C.case_tokenizer(c))
+    if "tokenized" in c:
+        assert np.array_equal(M.tokenized.numpy(), c["tokenized"])
     img = torch.from_numpy(batch.images)
     tr: dict = {}
     with torch.no_grad():
@@ -153,7 +155,7 @@ def test_synthetic_generator_is_counter_based():
     assert 0 <= u.min() and u.max() < 1 and abs(u.mean() - 0.5) < 0.01
 
 
-def test_tokenizer_semantics():
+def test_synthetic_tokenizer_semantics():
     t = syn.tokenize(["a photo of a forest.", "a photo of a dense residential."])
     assert t.shape == (2, 77) and t[0, 0] == syn.SOT_TOKEN
     eot = t.argmax(-1)
@@ -257,7 +259,7 @@ def test_oracle_caption_path_matches_reference(name):
     w, W, b = draw_caption_weights(torch.Generator().manual_seed(int(c["cap_seed"])))
     assert np.array_equal(w.float().numpy(), c["cap_w"]) and np.array_equal(b.float().numpy(), c["cap_b"])
     assert np.array_equal(W.double().reshape(-1).numpy()[c["cap_W_idx"]].astype(np.float32), c["cap_W_val"])
-    M = O.build_model(seed, J, names)
+    M = O.build_model(seed, J, names, tokenizer=C.case_tokenizer(c))
     tr: dict = {}
     caps = [str(x) for x in c["captions"]]
     loss = O.forward(M, torch.from_numpy(batch.images), torch.from_numpy(batch.labels), train=True, trace=tr,

@@ -10,8 +10,10 @@ engine (every op a libmapfed.so kernel) on them:
     relative L2 distance to the float64 restatement <= 1.25x the reference's own + 1e-4;
   * traced cases: every block output of both towers (clip/model.py:307-352), same bound per block; the
     table of ours-vs-reference, ours-vs-fp64 and reference-vs-fp64 per block is printed (DESIGN.md §5);
-  * gradient cases: every trainable gradient (relative L2 <= 5 %, norm within 3 %), the clip norm (1 %)
-    and the clip_grad_norm_ + SGD deltas (trainers/maple.py:586-598).
+  * gradient cases: every trainable gradient against the float64 restatement's, relative to the reference's
+    own fp16 distance: rel L2(ours, fp64) <= 1.25 x rel L2(reference, fp64) + 1e-3 per tensor (the fp16
+    floor the reference itself sits on; the fixture stores both), the clip norm (1 %) and the
+    clip_grad_norm_ + SGD deltas (trainers/maple.py:586-598).
 Set MAPFED_PARITY_REPORT=<dir> to write one JSON report per case."""
 import json
 import os
@@ -26,6 +28,7 @@ from federated_multi_modal_amd.engine import EngineConfig, MapleEngine
 pytestmark = pytest.mark.gpu
 
 FEAT_SLACK = 1e-4
+GRAD_RATIO, GRAD_SLACK = 1.25, 1e-3
 
 
 def _rel(a, b):
@@ -44,7 +47,10 @@ def _report(name, rep):
 def test_case_parity(name, dev):
     c = C.load_case(name)
     J, K, B, seed, names, batch = C.case_inputs(c)
-    e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed), device=dev)
+    e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed, bpe_path=C.case_bpe_path(c)),
+                    device=dev)
+    if "tokenized" in c:  # BPE cases: the class-prompt ids of the reference's own tokenizer
+        assert np.array_equal(e.tokenized.numpy(), c["tokenized"])
     e.load_batch(torch.from_numpy(batch.images), torch.from_numpy(batch.labels))
     logits = e.forward().float().cpu().numpy()
     rep = {"case": name, "J": J, "K": K, "B": B}
@@ -109,17 +115,24 @@ def test_case_parity(name, dev):
     loss_ok = abs(loss - float(c["loss"])) <= 2 * ulp
     if any(k.startswith("grad/norm/") for k in c):
         grads = {k: v.detach().double().cpu().reshape(-1).numpy() for k, v in e.grads().items()}
-        worst = []
+        worst, table = [], []
         for n in sorted(k[len("grad/norm/"):] for k in c if k.startswith("grad/norm/")):
             ours, ref = C.sel(c, "grad/", n, grads[n])
+            _, ref64 = C.sel(c, "grad64/", n, grads[n])
             rel = _rel(ours, ref)
-            nrm = abs(np.linalg.norm(grads[n]) - float(c[f"grad/norm/{n}"])) / (float(c[f"grad/norm/{n}"]) + 1e-30)
-            worst.append((rel, nrm, n))
-            if rel > 5e-2 or nrm > 3e-2:
-                grad_bad.append((n, rel, nrm))
+            o64, r64 = _rel(ours, ref64), _rel(ref, ref64)
+            ratio = o64 / max(r64, 1e-12)
+            table.append({"tensor": n, "vs_ref": rel, "ours_vs64": o64, "ref_vs64": r64})
+            worst.append((o64 - GRAD_RATIO * r64, ratio, rel, n))
+            if o64 > GRAD_RATIO * r64 + GRAD_SLACK:
+                grad_bad.append((n, o64, r64))
         worst.sort(reverse=True)
-        rep["grads_worst"] = [(n, a, b) for a, b, n in worst[:8]]
-        print(f"{name}: worst grads (rel L2, rel norm): {rep['grads_worst'][:4]}")
+        rep["grads"] = table
+        rep["grads_worst"] = [dict(tensor=n, ours64_over_ref64=r, vs_ref=v) for _, r, v, n in worst[:8]]
+        rep["grads_max_ratio"] = max(t["ours_vs64"] / max(t["ref_vs64"], 1e-12) for t in table)
+        rep["grads_max_vs_ref"] = max(t["vs_ref"] for t in table)
+        print(f"{name}: {len(table)} gradients; worst (ours-vs-fp64 / ref-vs-fp64, ours-vs-ref): "
+              f"{rep['grads_worst'][:4]}")
         before = {k: v.detach().double().cpu().reshape(-1).numpy() for k, v in e.trainable_state().items()}
         dtypes = {k: v.dtype for k, v in e.trainable_state().items()}
         e.set_lr(float(c["lr"]))

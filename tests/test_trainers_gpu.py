@@ -300,3 +300,81 @@ def test_disk_datasets_round(dev, tmp_path):
     tr.train()
     assert tr.nan_stats["total_updates"] == 1
     assert tr.clients[0]._cap_engine is not None  # captioned batches took the caption path
+
+
+class _Node(torch.nn.Module):
+    def forward(self, x):
+        return x
+
+
+def _torchscript_clip(tsd, path):
+    """A TorchScript archive with CLIP's parameter names (what clip._download fetches: a traced module
+    tree), written with torch.jit.save from tensors of our own."""
+    root = _Node()
+    for k, v in tsd.items():
+        parts, m = k.split("."), root
+        for p in parts[:-1]:
+            if p not in m._modules:
+                m.add_module(p, _Node())
+            m = m._modules[p]
+        m.register_parameter(parts[-1], torch.nn.Parameter(v.clone(), requires_grad=False))
+    torch.jit.save(torch.jit.trace(root, torch.zeros(1)), str(path))
+
+
+def test_torchscript_backbone_with_bpe_vocab(dev, tmp_path):
+    """MODEL.BACKBONE.PATH pointing at a TorchScript CLIP archive (the official file format; read by
+    clip_archive without running it) with CLIP's merges file beside it: the tower weights are the archive's,
+    and the class prompts / ctx init are tokenized with the byte-level BPE (trainers/maple.py:96-103,
+    136-143): the token ids equal the tokenizer's (pinned to the reference's SimpleTokenizer by
+    tests/test_tokenizer.py), the prefix / suffix rows and ctx are those ids' embedding rows."""
+    from federated_multi_modal_amd.tokenizer import BPE_FILE, get_tokenizer
+    sd = syn.clip_state_dict(11, full_token_table=True)
+    half = ("conv1.weight", "in_proj_weight", "in_proj_bias", "out_proj.weight", "out_proj.bias", "c_fc.weight",
+            "c_fc.bias", "c_proj.weight", "c_proj.bias", "visual.proj", "text_projection")
+    tsd = {k: torch.from_numpy(np.ascontiguousarray(v)).to(torch.float16 if k.endswith(half) else torch.float32)
+           for k, v in sd.items()}
+    (tmp_path / "ckpt").mkdir()
+    path = tmp_path / "ckpt" / "ViT-B-16.pt"
+    _torchscript_clip(tsd, path)
+    (tmp_path / "ckpt" / BPE_FILE).write_bytes((GOLD / "bpe_small_merges.txt.gz").read_bytes())
+    cfg = small_cfg(tmp_path, clients=1, epochs=1, extra=["MODEL.BACKBONE.PATH", str(path)])
+    tr = build_trainer(cfg)
+    e = tr.clients[0].engine
+    assert e.tokenizer.kind == "bpe"
+    assert torch.equal(e.P["image_encoder.transformer.resblocks.3.mlp.c_fc.weight"].cpu(),
+                       tsd["visual.transformer.resblocks.3.mlp.c_fc.weight"])
+    bpe = get_tokenizer(str(tmp_path / "ckpt" / BPE_FILE))
+    prompts = [f"a photo of a {c.replace('_', ' ')}." for c in e.cfg.classnames]
+    tok = torch.from_numpy(bpe.tokenize(prompts))
+    assert torch.equal(e.tokenized, tok)
+    table = tsd["token_embedding.weight"]
+    assert torch.equal(e.token_prefix.cpu(), table[tok[:, :1]].half())
+    assert torch.equal(e.token_suffix.cpu(), table[tok[:, 3:]].half())
+    init = torch.from_numpy(bpe.tokenize("a photo of a")[0, 1:3])
+    assert torch.equal(e.P["prompt_learner.ctx"].cpu(), table[init].half())
+    res = tr.clients[0].forward_backward(next(iter(tr.clients[0].dm.train_loader)))
+    assert np.isfinite(res["loss"])
+
+
+def test_caption_generator_shared_by_trainer_and_module(dev, tmp_path):
+    """One source for the caption path's random weights per client: the trainer's training step and
+    model(image, label, caption) both draw from model.caption_generator (the client's seeded generator), so
+    for the same seed the two entry points compute the same caption weights -- the same loss."""
+    from federated_multi_modal_amd.data import SyntheticClientDataManager
+    cfg = small_cfg(tmp_path, clients=1)
+    tr = build_trainer(cfg)
+    c = tr.clients[0]
+    assert c.model.caption_generator is c._cap_gen
+    c.dm = SyntheticClientDataManager(0, c.engine.cfg.classnames, n_train=4, n_test=4, train_batch=4, test_batch=4,
+                                      device=dev, seed=1, captions=True)
+    batch = next(iter(c.dm.train_loader))
+    state = c._cap_gen.get_state()
+    c.engine.clear_halt()
+    e = c._engine_for(batch["caption"])
+    c._load(batch["img"], batch["label"], e)
+    e.forward_backward()
+    loss_trainer = e.loss()
+    c._cap_gen.set_state(state)
+    c.model.train()
+    loss_module = float(c.model(batch["img"], batch["label"], batch["caption"]))
+    assert abs(loss_module - loss_trainer) <= 1e-6 * max(1.0, abs(loss_trainer))

@@ -50,9 +50,16 @@ def main(args):
         set_random_seed(cfg.SEED)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 and not torch.distributed.is_initialized():
+        # one rank per GPU over RCCL; MAPFED_DIST_BACKEND=gloo rehearses several ranks on one GPU
+        backend = os.environ.get("MAPFED_DIST_BACKEND", "nccl")
         local = int(os.environ.get("LOCAL_RANK", "0"))
+        if backend != "nccl":
+            local %= max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(backend)
     if int(os.environ.get("RANK", "0")) == 0:
         sys.stdout = _Tee(os.path.join(cfg.OUTPUT_DIR, "log.txt"))
     print(cfg)
