@@ -88,27 +88,33 @@ def cpu_baseline(J, K, B, budget_s=30.0, seed=0):
     img, lab = torch.from_numpy(b.images), torch.from_numpy(b.labels)
     ts = []
     t_all = time.perf_counter()
-    while len(ts) < 3 and (time.perf_counter() - t_all) < budget_s:
+    # one warm-up step, then at least 3 timed steps, more while the budget lasts
+    while len(ts) < 4 or (time.perf_counter() - t_all) < budget_s:
         t0 = time.perf_counter()
         O.train_step(M, img, lab, opt)
         ts.append(time.perf_counter() - t0)
         log(f"[bench] cpu step {len(ts)}: {ts[-1]:.1f}s")
-    sec = float(np.median(ts[1:])) if len(ts) > 1 else ts[0]
+        if len(ts) >= 8:
+            break
+    sec = float(np.median(ts[1:]))
     return {"value": Bs / sec, "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
             "cpu_model": cpu_model(),
-            "sample": f"{len(ts)} step(s) of one client at J={J}, B=1 image, K=1 class prompt "
-                      f"({sec:.2f} s/step{', median after the first' if len(ts) > 1 else ''}), torch-CPU fp16 "
+            "steps_timed": len(ts) - 1,
+            "sample": f"{len(ts)} steps of one client at J={J}, B=1 image, K=1 class prompt "
+                      f"({sec:.2f} s/step, median of the {len(ts) - 1} after the first), torch-CPU fp16 "
                       f"oracle, {torch.get_num_threads()} threads of {cpu_model()}; workload per-image work 87.6 vs "
                       f"{(B * FLOP_PER_IMAGE + K * FLOP_PER_CLASS) / B / 1e9:.1f} GFLOP"}
 
 
-def side_config(name, dev, world, rank, steps=5, warmup=2, seed=0):
+def side_config(name, dev, world, rank, steps=5, warmup=2, seed=0, eot_truncate=False, probe_gemm=True):
     """Another BASELINE config on the same ranks, reported beside `value` (never as it): the graph-replayed
     client step (fwd + bwd + clip + SGD) timed over `steps` steps (max over ranks), and the GEMM family
-    split by tower from one probed eager step (HIP events around every launch, towers serialised)."""
+    split by tower from one probed eager step (HIP events around every launch, towers serialised).
+    eot_truncate: the text tower on the first max(EOT)+1 tokens (the optional mode, never the value)."""
     J, K, B, desc = CONFIGS[name]
     names = syn.synthetic_classnames(K, seed)
-    e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed), device=dev)
+    e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed, eot_truncate=eot_truncate),
+                    device=dev)
     e.set_lr(0.0026)
     cb = syn.client_batch(seed, rank, 0, B, K)
     e.img_in.copy_(torch.from_numpy(cb.images))
@@ -130,21 +136,28 @@ def side_config(name, dev, world, rank, steps=5, warmup=2, seed=0):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     loss = e.loss()
-    probe = ops.KernelProbe("gemm")
-    e.overlap_towers = False
-    ops.set_probe(probe)
-    e.train_step()
-    ops.set_probe(None)
     fam = {}
-    for tower in ("text", "vision"):
-        p = probe.summary(f"gemm/{tower}")
-        fam[tower] = {"launches": p["launches"], "avg_launch_us": p["avg_us"], "tflops": p["tflops"],
-                      "mfma_frac": p["tflops"] * 1e12 / MFMA_PEAK_F16, "flop_per_launch": p["flops_per_launch"]}
+    if probe_gemm:
+        probe = ops.KernelProbe("gemm")
+        e.overlap_towers = False
+        ops.set_probe(probe)
+        e.train_step()
+        ops.set_probe(None)
+        for tower in ("text", "vision"):
+            p = probe.summary(f"gemm/{tower}")
+            fam[tower] = {"launches": p["launches"], "avg_launch_us": p["avg_us"], "tflops": p["tflops"],
+                          "mfma_frac": p["tflops"] * 1e12 / MFMA_PEAK_F16, "flop_per_launch": p["flops_per_launch"]}
     step_flop = B * FLOP_PER_IMAGE + K * FLOP_PER_CLASS
     out = {"workload": f"{name}: {desc}", "value": world * B * steps / el, "unit": "images/s",
            "ms_per_step": 1e3 * el / steps, "steps": steps, "loss": loss,
            "model_tflops": world * step_flop * steps / el / 1e12,
-           "model_mfma_frac": step_flop * steps / el / MFMA_PEAK_F16, "gemm_by_tower": fam}
+           "model_mfma_frac": step_flop * steps / el / MFMA_PEAK_F16, "gemm_by_tower": fam or None}
+    if eot_truncate:
+        Lt = e.text_len
+        out.update(text_tokens=Lt, executed_gflop_per_step=(B * FLOP_PER_IMAGE + K * text_flop_per_class(Lt)) / 1e9,
+                   algorithmic_gflop_per_step=step_flop / 1e9,
+                   parity="logits and loss bit-identical to the 77-token tower; gradients equal up to fp32 summation "
+                          "order (tests/test_engine_gpu.py::test_eot_truncated_text_tower_matches_full)")
     del g, e
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -499,6 +512,8 @@ def main():
     c5 = None
     if args.config == "c4" and not args.no_c5:
         c5 = side_config("c5", dev, world, rank)
+        if not args.no_eot_mode:  # where the optional mode matters: 1000 prompts of <= 10 tokens out of 77
+            c5["eot_truncated_mode"] = side_config("c5", dev, world, rank, eot_truncate=True, probe_gemm=False)
 
     out = {
         "metric": "images/sec/node (ViT-B/16 MaPLe fwd+bwd)",
@@ -520,6 +535,8 @@ def main():
         "fedavg_ms": fedavg_ms,
         "fedavg_mode": fed.mode,
         "fedavg_exposed_ms": fedavg_exposed_ms,
+        "fedavg_exposed_note": ("world 1: no collective (validity scan + pack + unpack only), nothing to hide"
+                                if world == 1 else f"{fed.mode} exchange over {world} ranks beside the last test()"),
         "fedavg_allreduce_ms": fedavg_allreduce_ms,
         "fedavg_bucket_mb": 4.0 * (eng.n16 + eng.n32 + 1) / 1e6,
         "fedavg_valid_clients": fed.n_valid(),

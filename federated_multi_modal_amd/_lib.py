@@ -25,6 +25,8 @@ SIGNATURES = {
     "mf_col_reduce_batch": [P, I, I, P],
     "mf_attention_fwd": [P, L, P, L, P, I, I, I, I, I, P],
     "mf_attention_bwd": [P, L, P, L, P, L, P, P, I, P, L, I, I, I, I, P],
+    "mf_qkv_attention_fwd": [P, L, I, P, P, P, L, P, L, P, I, I, I, I, I, P],
+    "mf_qkv_attention_supported": [I, I, I, I],
     "mf_im2col_patch": [P, I, P, I, I, I, P],
     "mf_vision_assemble": [P, P, P, P, P, I, I, I, I, P],
     "mf_text_assemble": [P, P, P, P, P, I, I, I, I, P],
@@ -64,7 +66,7 @@ SIGNATURES = {
 # functions that return a value, not a status
 _VALUE_FUNCS = {"mf_abi_version", "mf_layernorm_bwd_blocks", "mf_colsum_blocks", "mf_optim_chunk_bytes",
                 "mf_optim_chunk_elems", "mf_col_reduce_desc_bytes", "mf_small_linear_desc_bytes",
-                "mf_gemm_splitk_ws_floats", "mf_augment_ws_bytes"}
+                "mf_gemm_splitk_ws_floats", "mf_augment_ws_bytes", "mf_qkv_attention_supported"}
 # value functions whose return type is not int
 _RESTYPES = {"mf_augment_ws_bytes": ctypes.c_int64}
 

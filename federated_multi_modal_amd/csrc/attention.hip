@@ -404,6 +404,212 @@ __global__ __launch_bounds__(MAXT) void attn_fwd4_kernel(const f16* __restrict__
   MF_ASTAMP2(3);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused in-projection + attention forward: qkv_h = x_n W_h^T + b_h followed by SDPA on it
+// (ResidualAttentionBlock_MaPLe.attention -> nn.MultiheadAttention, clip/model.py:303-305: the
+// in-projection GEMM and the attention core of one block in one launch).
+//
+// One workgroup per (sequence n, head h).  Phase 1 is the head's slice of the in-projection GEMM:
+// [MR rows of x_n] x [192 rows of W_in: this head's q | k | v rows]^T, K = D, with the arithmetic of
+// the standalone GEMM (gemm.hip) -- v_mfma_f32_16x16x32_f16 with the weight fragment as the first
+// operand, k-subs of 32 in ascending k, fp16(acc + bias) -- so the q/k/v values are bit-identical to
+// mf_gemm_nt's.  Operands stream HBM -> LDS by LDS-DMA through a ring of NR k-sub slots ([rows][32]
+// images, 16-byte chunk c of row r at c ^ ((-(r >> 2)) & 3)), NR - 1 slots in flight.  Waves form a
+// (MR/32) x 2 grid of 32-row x 96-column sub-tiles.  Rows past the sequence read the next sequence's
+// rows (or zeros past the buffer): finite values whose keys the attention masks and whose queries are
+// not stored.  Phase 2 writes the fp16 q / k / v of the head into swizzled [MR][64] LDS images (the
+// ring is dead by then), stores them to `qkv` (the backward reads them), and runs the attention of
+// fwd4_tile on them: one 16-query tile per wave, bit-identical to attn_fwd4_kernel.
+// What the fusion removes: the qkv round trip through HBM between the two launches (the attention's
+// K / V staging burst), one launch boundary, and the GEMM's chip-wide epilogue store burst (here the
+// stores of a head overlap other workgroups' GEMM phases).
+MF_DEV void wait_vm_n(int n) {  // s_waitcnt vmcnt(n), n wave-uniform in 0..15
+  switch (n) {
+#define MF_VMC(k) case k: __builtin_amdgcn_s_waitcnt((k & 15) | (7 << 4) | (15 << 8)); break;
+    MF_VMC(0) MF_VMC(1) MF_VMC(2) MF_VMC(3) MF_VMC(4) MF_VMC(5) MF_VMC(6) MF_VMC(7)
+    MF_VMC(8) MF_VMC(9) MF_VMC(10) MF_VMC(11) MF_VMC(12) MF_VMC(13) MF_VMC(14) MF_VMC(15)
+#undef MF_VMC
+    default: __builtin_amdgcn_s_waitcnt((0 & 15) | (7 << 4) | (15 << 8)); break;
+  }
+}
+
+MF_DEV void lds_bar() {  // s_barrier with LDS ordering and no vmcnt(0): LDS-DMA stays in flight across it
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// one k-sub of the fused kernel's LDS-DMA: this wave's instructions u (x rows or W rows) into `slot`.  The
+// buffer descriptors are built here from (pointer, byte range): a kernel template whose body holds a
+// descriptor-typed lambda capture or parameter loses its host stub under hipcc (see gemm.hip dma_stage).
+template <int IPW_MAX, int NW, int NI>
+MF_DEV void qkv_dma_issue(const f16* x, int x_bytes, const f16* w, int w_bytes, f16* slot, const int* voff,
+                          const int* dst, const bool* isx, int kbytes, int wid) {
+  const auto x_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, x_bytes, 0x00020000);
+  const auto w_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)w, 0, w_bytes, 0x00020000);
+#pragma unroll
+  for (int u = 0; u < IPW_MAX; ++u) {
+    if (wid + NW * u < NI) {
+      if (isx[u])
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(x_rsrc, (lds_ptr_t)(slot + dst[u]), 16, voff[u] + kbytes, 0, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rsrc, (lds_ptr_t)(slot + dst[u]), 16, voff[u] + kbytes, 0, 0, 0);
+    }
+  }
+}
+
+template <int LKP, int MR, int D, bool CAUSAL, int NR>
+__global__ __launch_bounds__(MR / 32 * 2 * 64) void qkv_attn_fwd_kernel(
+    const f16* __restrict__ x, int64_t ld_x, int x_rows, const f16* __restrict__ w, const f16* __restrict__ bias,
+    f16* __restrict__ qkv, int64_t ld_qkv, f16* __restrict__ out, int64_t ld_out, float* __restrict__ lse,
+    int ld_lse, int L, int H) {
+  constexpr int WMG = MR / 32, NW = 2 * WMG, NT = 64 * NW;
+  constexpr int HK = 32, KS = 64, NKT = D / KS;  // k-subs of 32; a K-step (ring slot) holds two
+  constexpr int NA = MR / 16, NB = 192 / 16;     // LDS-DMA wave instructions (16 rows x 64 B) per k-sub
+  constexpr int NI = NA + NB;
+  constexpr int IPW_MAX = (NI + NW - 1) / NW;
+  constexpr int HALF = (MR + 192) * HK;          // one k-sub's [A | B] images
+  constexpr int SLOT = 2 * HALF;                 // fp16 elements per ring slot (one K-step)
+  constexpr int IMG = MR * 64;                   // one [MR][64] q / k / v image
+  constexpr int RING = NR * SLOT;
+  constexpr int LDS_ELEMS = RING > 3 * IMG ? RING : 3 * IMG;
+  constexpr int P = NR - 1;                      // K-steps in flight
+  static_assert(LDS_ELEMS * 2 <= 160 * 1024, "LDS");
+  static_assert(LKP <= MR && LKP % 16 == 0 && LKP / 16 <= NW, "one attention tile per wave");
+  static_assert(2 * IPW_MAX * (P - 1) <= 15, "vmcnt range");
+  __shared__ __attribute__((aligned(1024))) f16 lds[LDS_ELEMS];
+
+  // XCD-aware bijective remap (blocks are dealt round-robin over the 8 XCDs): each XCD takes a contiguous
+  // range of (sequence, head) pairs, so the 12 heads of a sequence share its x rows in one L2
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int nh = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int n = nh / H, h = nh % H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mg = wid >> 1, ng = wid & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+
+  // LDS-DMA plan: wave instruction t (t = wid + NW*u) fills 16 rows of the slot: t < NA -> x rows
+  // 16t.., else W rows of part (t-NA)/4 (q, k, v), 16 rows each
+  const int x_bytes = (int)(((int64_t)(x_rows - 1) * ld_x + D) * 2);
+  const int w_bytes = (int)(((int64_t)3 * D - 1) * D + D) * 2;
+  const int src_chunk = (lane & 3) ^ ((-(lane >> 4)) & 3);
+  int dma_voff[IPW_MAX], dma_dst[IPW_MAX];
+  bool dma_x[IPW_MAX];
+  int ipw = 0;
+#pragma unroll
+  for (int u = 0; u < IPW_MAX; ++u) {
+    const int t = wid + NW * u;
+    dma_x[u] = t < NA;
+    if (t < NA) {
+      const int row = 16 * t + (lane >> 2);
+      dma_voff[u] = (int)((((int64_t)n * L + row) * ld_x + src_chunk * 8) * 2);
+      dma_dst[u] = 16 * t * HK;
+    } else {
+      const int tb = t - NA, part = tb >> 2;
+      const int wrow = part * D + h * 64 + 16 * (tb & 3) + (lane >> 2);
+      dma_voff[u] = (int)(((int64_t)wrow * D + src_chunk * 8) * 2);
+      dma_dst[u] = (MR + 16 * tb) * HK;
+    }
+    ipw += t < NI ? 1 : 0;
+  }
+#define MF_QKV_ISSUE(kt)                                                                                     \
+  do {                                                                                                       \
+    f16* s_ = lds + ((kt) % NR) * SLOT;                                                                      \
+    qkv_dma_issue<IPW_MAX, NW, NI>(x, x_bytes, w, w_bytes, s_, dma_voff, dma_dst, dma_x, (kt) * KS * 2, wid); \
+    qkv_dma_issue<IPW_MAX, NW, NI>(x, x_bytes, w, w_bytes, s_ + HALF, dma_voff, dma_dst, dma_x,              \
+                                   (kt) * KS * 2 + HK * 2, wid);                                             \
+  } while (0)
+
+  // bias of this lane's output columns (read before the DMA stream, so the first retire covers it)
+  f16x4 bv[6];
+#pragma unroll
+  for (int jj = 0; jj < 6; ++jj) {
+    const int j = 6 * ng + jj;
+    bv[jj] = *(const f16x4*)(bias + (j >> 2) * D + h * 64 + 16 * (j & 3) + 4 * fg);
+  }
+  f32x4 acc[2][6];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 6; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  MF_ASTAMP2(0);
+#pragma unroll
+  for (int kt = 0; kt < P; ++kt) MF_QKV_ISSUE(kt);
+  const int frag_off = fr * HK + ((fg ^ ((-(fr >> 2)) & 3)) << 3);
+#pragma unroll 1
+  for (int kt = 0; kt < NKT; ++kt) {
+    // this wave's DMA of K-step kt landed (the younger in-flight K-steps may stay), then every wave's
+    wait_vm_n(2 * ipw * min(P - 1, NKT - 1 - kt));
+    lds_bar();
+    if (kt + P < NKT) MF_QKV_ISSUE(kt + P);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {  // k-subs in ascending k (the standalone GEMM's accumulation order)
+      const f16* sa = lds + (kt % NR) * SLOT + s * HALF;
+      const f16* sb = sa + MR * HK;
+      f16x8 af[2], bf[6];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = *(const f16x8*)(sa + (32 * mg + 16 * i) * HK + frag_off);
+#pragma unroll
+      for (int jj = 0; jj < 6; ++jj) bf[jj] = *(const f16x8*)(sb + (16 * (6 * ng + jj)) * HK + frag_off);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 6; ++jj)
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[jj], af[i], acc[i][jj], 0, 0, 0);
+    }
+  }
+  MF_ASTAMP2(1);
+  __syncthreads();  // every wave is done with the ring
+
+  // q / k / v images: fp16(acc + bias) (the GEMM's EPI_BIAS rounding); lane holds row
+  // 32mg + 16i + fr, columns 16j + 4fg .. +3 of the head's 192
+  f16* sQ = lds;
+  f16* sK = lds + IMG;
+  f16* sV = lds + 2 * IMG;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 32 * mg + 16 * i + fr;
+#pragma unroll
+    for (int jj = 0; jj < 6; ++jj) {
+      const int j = 6 * ng + jj;
+      f16x4 t;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[e] = (f16)(acc[i][jj][e] + (float)bv[jj][e]);
+      *(f16x4*)(lds + (j >> 2) * IMG + sw_off(r, 16 * (j & 3) + 4 * fg)) = t;
+    }
+  }
+  __syncthreads();
+  MF_ASTAMP2(2);
+  // the head's q | k | v rows to HBM (the backward's operands), 16 B per access
+  for (int t = tid; t < L * 24; t += NT) {
+    const int r = t / 24, pc = t - 24 * r, part = pc >> 3, c = pc & 7;
+    const f16x8 v = *(const f16x8*)(lds + part * IMG + sw_off(r, 8 * c));
+    *(f16x8*)(qkv + ((int64_t)n * L + r) * ld_qkv + part * D + h * 64 + 8 * c) = v;
+  }
+  // attention: wave w takes queries 16w .. 16w+15
+  if (wid < LKP / 16) {
+    const int q0 = 16 * wid, ii = lane & 15;
+    int koff[4], voff[8];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int row = 16 * hf + fr;
+        koff[2 * s2 + hf] = row * 64 + (((4 * s2 + fg) ^ (row & 7)) << 3);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) voff[2 * dt + hf] = sw_off(16 * hf + 4 * fg + (ii >> 2), 16 * dt + 4 * (ii & 3));
+    }
+    const f16x8 qf0 = ld_frag(sQ, q0 + fr, fg), qf1 = ld_frag(sQ, q0 + fr, 4 + fg);
+    fwd4_tile<LKP, CAUSAL, false>(sK, sV, koff, voff, qf0, qf1, true, q0, L, lane, out, ld_out, lse, ld_lse,
+                                  (int64_t)n * L, h, nh);
+  }
+  MF_ASTAMP2(3);
+}
+
 // Dq[nh][q] = sum_d dO[q][d] * O[q][d] (fp32) ------------------------------------------------
 __global__ void attn_bwd_dot_kernel(const f16* __restrict__ out, int64_t ld_out, const f16* __restrict__ dout,
                                     int64_t ld_dout, float* __restrict__ dq_dot, int ld_lse, int N, int L, int H) {
@@ -1021,4 +1227,37 @@ extern "C" int mf_attention_bwd(const void* qkv, int64_t ld_qkv, const void* out
 #undef CALLB
   MF_CHECK_LAUNCH();
   return 0;
+}
+
+// qkv = x W_in^T + b_in (fp16, bias epilogue) and out / lse = SDPA(qkv) in one launch (qkv_attn_fwd_kernel):
+// the vision tower's blocks (D = 768, 193..208 tokens) and the text tower's (D = 512, causal, 65..80 tokens)
+extern "C" int mf_qkv_attention_fwd(const void* x, int64_t ld_x, int x_rows, const void* w, const void* bias,
+                                    void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* lse, int ld_lse,
+                                    int N, int L, int H, int causal, void* stream) {
+  if (N <= 0) return 0;
+  const int D = H * 64;
+  if ((ld_x % 8) || (ld_qkv % 8) || (ld_out % 4) || ld_lse < L || ld_x < D || ld_qkv < 3 * D ||
+      (uintptr_t)x % 16 || (uintptr_t)w % 16 || (uintptr_t)qkv % 16 || (uintptr_t)bias % 8)
+    return mf_set_error("mf_qkv_attention_fwd: bad strides / alignment", -1);
+  if (x_rows < N * L) return mf_set_error("mf_qkv_attention_fwd: x has fewer than N*L rows", -1);
+  hipStream_t st = (hipStream_t)stream;
+  if (D == 768 && !causal && L > 192 && L <= 208) {
+    qkv_attn_fwd_kernel<208, 224, 768, false, 3><<<N * H, 896, 0, st>>>(
+        (const f16*)x, ld_x, x_rows, (const f16*)w, (const f16*)bias, (f16*)qkv, ld_qkv, (f16*)out, ld_out, lse,
+        ld_lse, L, H);
+  } else if (D == 512 && causal && L > 64 && L <= 80) {
+    qkv_attn_fwd_kernel<80, 96, 512, true, 2><<<N * H, 384, 0, st>>>(
+        (const f16*)x, ld_x, x_rows, (const f16*)w, (const f16*)bias, (f16*)qkv, ld_qkv, (f16*)out, ld_out, lse,
+        ld_lse, L, H);
+  } else {
+    return mf_set_error("mf_qkv_attention_fwd: shape outside the fused kernels (vision D=768 L 193..208, text "
+                        "D=512 causal L 65..80)", -1);
+  }
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mf_qkv_attention_supported(int N, int L, int H, int causal) {
+  const int D = H * 64;
+  return N > 0 && ((D == 768 && !causal && L > 192 && L <= 208) || (D == 512 && causal && L > 64 && L <= 80));
 }

@@ -35,6 +35,9 @@ from .tokenizer import get_tokenizer
 
 F16, F32 = torch.float16, torch.float32
 N_CTX = 2
+# towers whose in-projection + attention forward run as one launch by default (MAPFED_FUSED_QKV_ATTN
+# overrides: "1" both, "0" neither, "vision" / "text" one); chosen by the same-box A/B in DESIGN.md §6
+FUSED_QKV_ATTN_DEFAULT = "0"
 
 
 @dataclass
@@ -288,6 +291,10 @@ class _Tower:
         self.dQKV = e(R, 3 * D)
         self.dF = e(R, 4 * D)
         self.attn_ws = e(N * H * max(self.Ls), dt=F32)
+        # the in-projection + attention forward as one launch (mf_qkv_attention_fwd) where its shapes allow;
+        # MAPFED_FUSED_QKV_ATTN=0 selects the unfused pair (A/B), "vision" / "text" fuses that tower only
+        sel = os.environ.get("MAPFED_FUSED_QKV_ATTN", FUSED_QKV_ATTN_DEFAULT)
+        self.fused_qkv_attn = sel == "1" or ("vision" if name == "image_encoder" else "text") in sel.split(",")
         # this tower's LayerNorm dgamma/dbeta partials, reduced in one launch at the end of its backward
         self.lnb = ops.LNGradBatch(dev)
         self.cs_ws = e(ops.colsum_ws_floats(R, 4 * D), dt=F32)
@@ -326,9 +333,14 @@ class _Tower:
             else:
                 ops.layernorm_fwd(x, self.p(i, "ln_1.weight"), self.p(i, "ln_1.bias"), h1, self.mean1[i],
                                   self.rstd1[i])
-            ops.gemm_nt(h1, self.p(i, "attn.in_proj_weight"), self.QKV[i], bias=self.p(i, "attn.in_proj_bias"),
-                        epilogue=ops.EPI_BIAS)
-            ops.attention_fwd(self.QKV[i], N, L, H, self.causal, out=self.O[i], lse=self.LSE[i])
+            if self.fused_qkv_attn and ops.qkv_attention_supported(N, L, H, self.causal):
+                # in-projection + attention in one launch (bit-identical to the pair below)
+                ops.qkv_attention_fwd(h1, self.p(i, "attn.in_proj_weight"), self.p(i, "attn.in_proj_bias"),
+                                      self.QKV[i], self.O[i], self.LSE[i], N, L, H, self.causal)
+            else:
+                ops.gemm_nt(h1, self.p(i, "attn.in_proj_weight"), self.QKV[i], bias=self.p(i, "attn.in_proj_bias"),
+                            epilogue=ops.EPI_BIAS)
+                ops.attention_fwd(self.QKV[i], N, L, H, self.causal, out=self.O[i], lse=self.LSE[i])
             ops.gemm_nt(self.O[i], self.p(i, "attn.out_proj.weight"), self.X1[i], bias=self.p(i, "attn.out_proj.bias"),
                         aux_in=x, epilogue=ops.EPI_BIAS_RESID)
             h2 = self.H2[:R]

@@ -124,15 +124,23 @@ class Transformer(nn.Module):
     def forward(self, inputs):
         return self.resblocks(inputs)
 
-    def rows(self, x: torch.Tensor, N: int, L: int, deep: List[torch.Tensor]) -> torch.Tensor:
+    def rows(self, x: torch.Tensor, N: int, L: int, deep: List[torch.Tensor],
+             cap: Optional[torch.Tensor] = None):
+        """The blocks on NLD rows; returns (rows, final sequence length).  cap [ncap, D] fp16 (the caption
+        path's projected rows, clip/model.py:550-561): each prompted block's input keeps all but the last
+        n_ctx rows of the previous output and appends cap + the deep prompt, so the sequence grows by ncap."""
         counter = 0
         for i, blk in enumerate(self.resblocks):
             prompt = None
             if i > 0 and len(deep) > 0 and not counter > len(deep) - 1:
                 prompt = deep[counter]
                 counter += 1
+            if prompt is not None and cap is not None:
+                grown = torch.empty(N * (L + cap.shape[0]), x.shape[1], device=x.device, dtype=F16)
+                ops.seq_grow(x, grown, cap, prompt.float().contiguous(), N, L, cap.shape[0], N_CTX, x.shape[1])
+                x, L, prompt = grown, L + cap.shape[0], None
             x = blk.rows(x, N, L, prompt)
-        return x
+        return x, L
 
 
 class VisionTransformer(nn.Module):
@@ -158,12 +166,28 @@ class VisionTransformer(nn.Module):
         self.ln_post = _Holder()
         self.ln_post.weight = _param(engine, ie + "ln_post.weight", cache)
         self.ln_post.bias = _param(engine, ie + "ln_post.bias", cache)
+        self.caption_generator: Optional[torch.Generator] = None  # None: torch's global generator
+
+    def caption_rows(self, clip_embeddings: torch.Tensor) -> torch.Tensor:
+        """clip/model.py:550-558: AttentionPooling with a fresh random vector, then a fresh random
+        Linear(512, 768), both fp16 and drawn (in the reference's order) from the generator CustomCLIP names
+        (torch's global one by default): [ncap, 77, 512] token embeddings -> [ncap, 768]."""
+        emb = clip_embeddings.to(device=self.conv1.weight.device, dtype=F16).contiguous()
+        ncap, T, Dt = emb.shape
+        gen = self.caption_generator if self.caption_generator is not None else torch.default_generator
+        w, W, b = draw_caption_weights(gen, Dt, self.width)
+        dev = emb.device
+        pooled = torch.empty(ncap, Dt, device=dev, dtype=F16)
+        # the pooling kernel gathers rows by token id: here every caption's own rows, in order
+        ids = torch.arange(ncap * T, device=dev, dtype=torch.int32).view(ncap, T)
+        ops.caption_pool(ids, emb.view(ncap * T, Dt).float(), w.to(dev), pooled)
+        return ops.gemm_nt(pooled, W.to(dev), bias=b.to(dev), epilogue=ops.EPI_BIAS)
 
     @torch.no_grad()
     def forward(self, x: torch.Tensor, shared_ctx: torch.Tensor, compound_deeper_prompts, clip_embeddings=None):
-        if clip_embeddings is not None:
-            raise NotImplementedError("caption-conditioned visual prompts (clip/model.py:550-561) are not on this "
-                                      "module path; pass caption=None")
+        """clip/model.py:509-572.  clip_embeddings [ncap, 77, 512] (the caption tokens' embedding): the
+        caption-conditioned visual prompts, each prompted block's sequence growing by ncap rows."""
+        cap = self.caption_rows(clip_embeddings) if clip_embeddings is not None else None
         B = x.shape[0]
         G2, D, p = self.grid * self.grid, self.width, self.patch
         L = G2 + 1 + N_CTX
@@ -177,7 +201,7 @@ class VisionTransformer(nn.Module):
         ops.vision_assemble(patch, self.class_embedding, self.positional_embedding, shared_ctx.to(F16).contiguous(),
                             xpre, B, G2, N_CTX, D)
         h, _, _ = ops.layernorm_fwd(xpre, self.ln_pre.weight, self.ln_pre.bias)
-        h = self.transformer.rows(h, B, L, list(compound_deeper_prompts))
+        h, L = self.transformer.rows(h, B, L, list(compound_deeper_prompts), cap)
         cls_rows = torch.arange(0, B * L, L, dtype=torch.int32, device=img.device)
         post, _, _ = ops.layernorm_fwd(h, self.ln_post.weight, self.ln_post.bias, row_index=cls_rows)
         return ops.gemm(post, self.proj, epilogue=ops.EPI_NONE, b_kmajor=True)
@@ -202,7 +226,7 @@ class TextEncoder(nn.Module):
     def forward(self, prompts: torch.Tensor, tokenized_prompts: torch.Tensor, compound_prompts_deeper_text):
         K, L, D = prompts.shape
         x = (prompts.to(F16) + self.positional_embedding.to(F16)).contiguous().view(K * L, D)
-        x = self.transformer.rows(x, K, L, list(compound_prompts_deeper_text))
+        x, _ = self.transformer.rows(x, K, L, list(compound_prompts_deeper_text))
         eot = tokenized_prompts.to(x.device).argmax(dim=-1).to(torch.int64)
         rows = (torch.arange(K, device=x.device, dtype=torch.int64) * L + eot).to(torch.int32)
         fin, _, _ = ops.layernorm_fwd(x, self.ln_final.weight, self.ln_final.bias, row_index=rows)
@@ -315,7 +339,17 @@ class CustomCLIP(nn.Module):
         # where the caption path's random AttentionPooling / Linear weights come from: torch's global CPU
         # generator, as in the reference (clip/model.py:461, 557); the federated trainer assigns each client
         # its own seeded generator here, and its training step draws from the same attribute
-        self.caption_generator: torch.Generator = torch.default_generator
+        self.caption_generator = torch.default_generator
+
+    @property
+    def caption_generator(self) -> torch.Generator:
+        return self.__dict__["_caption_generator"]
+
+    @caption_generator.setter
+    def caption_generator(self, gen: torch.Generator):
+        self.__dict__["_caption_generator"] = gen
+        if "image_encoder" in self._modules:
+            self.image_encoder.caption_generator = gen
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         """nn.Module.load_state_dict semantics on the engine (MapleEngine.load_state_dict: strict key check

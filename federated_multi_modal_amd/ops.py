@@ -321,6 +321,32 @@ def attention_fwd(qkv, N, L, H, causal, out=None, lse=None, ld_lse=None):
     return out, lse
 
 
+def qkv_attention_supported(N, L, H, causal) -> bool:
+    return bool(call("mf_qkv_attention_supported", N, L, H, int(causal)))
+
+
+def qkv_attention_fwd(x, w, bias, qkv, out, lse, N, L, H, causal, ld_lse=None):
+    """The in-projection (qkv = x w^T + bias, fp16) and the attention forward in one launch
+    (mf_qkv_attention_fwd): qkv [N*L, 3D] is written too (the backward reads it)."""
+    D = H * 64
+    if ld_lse is None:
+        ld_lse = L
+    assert x.shape[1] == D and tuple(w.shape) == (3 * D, D) and bias.numel() == 3 * D
+    ev = None
+    if _PROBE is not None and _PROBE.wants("attention"):
+        # algorithmic: the in-projection 2 * (N*L) * 3D * D plus QK^T + PV; bytes: x and W read, qkv, O (fp16)
+        # and the LSE written -- the round trip of qkv between two launches is gone
+        pairs = L * (L + 1) / 2 if causal else L * L
+        flops = 2.0 * N * L * 3 * D * D + 4.0 * N * H * pairs * 64
+        nbytes = 2.0 * N * L * D + 2.0 * 3 * D * D + 2.0 * N * L * 3 * D + 2.0 * N * L * D + 4.0 * N * H * L
+        ev = _PROBE.around(flops, nbytes, f"attention_fused_fwd/L{L}")
+    call("mf_qkv_attention_fwd", _p(x), _ld(x), x.shape[0], _p(w), _p(bias), _p(qkv), _ld(qkv), _p(out), _ld(out),
+         _p(lse), ld_lse, N, L, H, int(causal), _s())
+    if ev is not None:
+        ev.record()
+    return out, lse
+
+
 def attention_bwd(qkv, out, dout, lse, N, L, H, causal, dqkv=None, ws=None, ld_lse=None):
     if ld_lse is None:
         ld_lse = L

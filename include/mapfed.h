@@ -92,10 +92,21 @@ int mf_layernorm_bwd_inject(const void* dy, int64_t lddy, const void* x, int64_t
 int mf_col_reduce_desc_bytes(void);
 int mf_col_reduce_batch(const void* descs, int n, int max_cols, void* stream);
 
-/* ---- attention (head_dim 64, L <= 256; SDPA inside nn.MultiheadAttention, clip/model.py:303-305,
- * causal mask clip/model.py:679-685) — qkv [N*L, 3*H*64], out [N*L, H*64], lse [N*H, ld_lse]       */
+/* ---- attention (head_dim 64, L <= 512: one-pass kernels up to 256 rows, the caption path's growing
+ * vision sequences of 257..512 rows on the two-pass forward / dK-dV + dQ backward; SDPA inside
+ * nn.MultiheadAttention, clip/model.py:303-305, causal mask clip/model.py:679-685)
+ * — qkv [N*L, 3*H*64], out [N*L, H*64], lse [N*H, ld_lse]                                         */
 int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* lse, int ld_lse, int N,
                      int L, int H, int causal, void* stream);
+/* The in-projection and the attention forward in one launch: qkv = fp16(x w^T + bias) (w = in_proj_weight
+ * [3D, D], bias [3D]; bit-identical to mf_gemm_nt's EPI_BIAS) is written to qkv [N*L, 3D] and attended
+ * as mf_attention_fwd does (bit-identical out / lse).  Shapes: the vision blocks (D = 768, 193..208
+ * tokens) and the text blocks (D = 512, causal, 65..80 tokens); x_rows = rows of the x buffer (>= N*L).
+ * Replaces the in_proj + SDPA of nn.MultiheadAttention (clip/model.py:303-305).                      */
+int mf_qkv_attention_fwd(const void* x, int64_t ld_x, int x_rows, const void* w, const void* bias, void* qkv,
+                         int64_t ld_qkv, void* out, int64_t ld_out, float* lse, int ld_lse, int N, int L, int H,
+                         int causal, void* stream);
+int mf_qkv_attention_supported(int N, int L, int H, int causal);
 /* dqkv [N*L, 3*H*64]; dq_dot_ws: N*H*ld_lse floats of workspace                                   */
 int mf_attention_bwd(const void* qkv, int64_t ld_qkv, const void* out, int64_t ld_out, const void* dout,
                      int64_t ld_dout, const float* lse, float* dq_dot_ws, int ld_lse, void* dqkv, int64_t ld_dqkv,

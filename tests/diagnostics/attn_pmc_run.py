@@ -1,6 +1,7 @@
 """Diagnostic (GPU box): eager attention launches on the c4 shapes for PMC passes
 (scripts/attn_pmc.sh -> tests/diagnostics/attn_pmc_summary.py).  Vision N=32 L=199 H=12 and text
-K=38 L=77 H=8 causal, forward and backward, 5 launches each after one warm-up; no hipGraph, so every
+K=38 L=77 H=8 causal, forward and backward, and the fused in-projection + attention forward
+(qkv_attn_fwd_kernel), 5 launches each after one warm-up; no hipGraph, so every
 dispatch is seen by the counter collection."""
 import sys
 from pathlib import Path
@@ -19,8 +20,12 @@ for (N, L, H, causal) in [(32, 199, 12, False), (38, 77, 8, True)]:
     dout = torch.randn(N * L, D, device=dev).half()
     dqkv = torch.empty_like(qkv)
     ws = torch.empty(N * H * L, device=dev)
+    x = torch.randn(N * L, D, device=dev).half()
+    W = (torch.randn(3 * D, D, device=dev) * D ** -0.5).half()
+    b = (torch.randn(3 * D, device=dev) * 0.02).half()
     for _ in range(6):
         ops.attention_fwd(qkv, N, L, H, causal, out=out, lse=lse)
         ops.attention_bwd(qkv, out, dout, lse, N, L, H, causal, dqkv=dqkv, ws=ws)
+        ops.qkv_attention_fwd(x, W, b, qkv, out, lse, N, L, H, causal)  # the fused in-projection + attention
     torch.cuda.synchronize()
     print(f"N={N} L={L} H={H} causal={causal}: done", flush=True)

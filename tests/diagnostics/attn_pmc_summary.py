@@ -22,10 +22,10 @@ SHAPES = {  # launches of tests/diagnostics/attn_pmc_run.py: rows x heads -> (N,
 
 
 def short(name: str) -> str:
-    d = re.search(r"(attn_\w+?_kernel)<([^>]*)>", name)  # demangled
+    d = re.search(r"((?:qkv_)?attn_\w+?_kernel)<([^>]*)>", name)  # demangled
     if d:
         return d.group(1) + "<" + d.group(2).replace(" ", "") + ">"
-    m = re.search(r"(attn_\w+?_kernel)I(.*?)EEEv", name)  # mangled
+    m = re.search(r"((?:qkv_)?attn_\w+?_kernel)I(.*?)EEEv", name)  # mangled
     if not m:
         return name[:60]
     args = re.findall(r"Li(\d+)|Lb(\d)", m.group(2))
@@ -70,6 +70,9 @@ def main():
             per_row = (2 * 8 * 64 + 4) if "bwd" in k else (2 * 4 * 64 + 4)
             r["tower"] = tower
             r["algorithmic_bytes"] = N * H * L * per_row
+            if k.startswith("qkv_attn"):  # x and W read once, qkv + O written (fp16), LSE (fp32)
+                D = 64 * H
+                r["algorithmic_bytes"] = 2 * N * L * D + 2 * 3 * D * D + 2 * N * L * 4 * D + 4 * N * H * L
             if "read_bytes" in r and "write_bytes" in r:
                 r["traffic_over_algorithmic"] = (r["read_bytes"] + r["write_bytes"]) / r["algorithmic_bytes"]
         res[f"{k} grid={grid}"] = r

@@ -337,3 +337,29 @@ def test_c5_full_size_properties(dev):
     assert all(torch.equal(g0[k], g1[k]) for k in g0) and all(torch.equal(p0[k], p1[k]) for k in p0)
     assert all(torch.isfinite(v.float()).all() for v in g0.values())
     assert torch.equal(l0, l2) and s0 == s2
+
+
+def test_fused_qkv_attention_does_not_change_results(dev, monkeypatch):
+    """The in-projection + attention forward as one launch (MAPFED_FUSED_QKV_ATTN, on by default for both
+    towers) against the unfused pair: logits, loss and every gradient bit-identical at the c4 client shape
+    (J = 9, K = 38, B = 32)."""
+    J, K, B, seed = 9, 38, 32, 2
+    names = syn.synthetic_classnames(K, seed)
+    b = syn.client_batch(seed, 0, 0, B, K)
+    out = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("MAPFED_FUSED_QKV_ATTN", fused)
+        e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed), device=dev)
+        assert e.vis.fused_qkv_attn == (fused == "1") and e.txt.fused_qkv_attn == (fused == "1")
+        e.load_batch(torch.from_numpy(b.images), torch.from_numpy(b.labels))
+        logits = e.forward().clone()
+        e.forward_backward()
+        out.append((logits, e.loss(), {k: v.detach().clone() for k, v in e.grads().items()},
+                    e.vis.QKV[3].clone(), e.txt.O[5].clone()))
+        del e
+        torch.cuda.empty_cache()
+    (lg0, l0, g0, q0, o0), (lg1, l1, g1, q1, o1) = out
+    assert torch.equal(lg0, lg1) and l0 == l1
+    assert torch.equal(q0, q1) and torch.equal(o0, o1)
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n

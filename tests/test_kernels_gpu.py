@@ -271,6 +271,31 @@ def test_attention_fwd_bwd(dev, N, L, H, causal):
     assert rel < 5e-3, rel
 
 
+@pytest.mark.parametrize("N,L,H,causal", [(4, 199, 12, False), (32, 199, 12, False), (3, 193, 12, False),
+                                          (38, 77, 8, True), (5, 80, 8, True)])
+def test_qkv_attention_fused_matches_unfused(dev, N, L, H, causal):
+    """mf_qkv_attention_fwd (in-projection + attention in one launch) against the two launches it replaces
+    (mf_gemm_nt with the bias epilogue, then mf_attention_fwd): qkv, out and lse bit-identical (same MFMA,
+    same k order, same fp16 rounding points), incl. the last sequence of the buffer (rows past it read as 0)."""
+    D = H * 64
+    g = torch.Generator(device="cpu").manual_seed(N * 1000 + L)
+    x = torch.randn(N * L, D, generator=g).half().to(dev)
+    W = (torch.randn(3 * D, D, generator=g) * D ** -0.5).half().to(dev)
+    b = (torch.randn(3 * D, generator=g) * 0.02).half().to(dev)
+    qkv_ref = ops.gemm_nt(x, W, bias=b, epilogue=ops.EPI_BIAS)
+    o_ref, lse_ref = ops.attention_fwd(qkv_ref, N, L, H, causal)
+    assert ops.qkv_attention_supported(N, L, H, causal)
+    qkv = torch.full_like(qkv_ref, float("nan"))
+    o = torch.full((N * L, D), float("nan"), device=dev, dtype=torch.float16)
+    lse = torch.full((N * H * L,), float("nan"), device=dev, dtype=torch.float32)
+    ops.qkv_attention_fwd(x, W, b, qkv, o, lse, N, L, H, causal)
+    torch.cuda.synchronize()
+    assert torch.equal(qkv, qkv_ref)
+    assert torch.equal(o, o_ref)
+    assert torch.equal(lse, lse_ref)
+    assert not ops.qkv_attention_supported(N, 10, H, causal)  # the EOT-truncated text tower stays unfused
+
+
 def test_assemble_inject_transpose_colsum(dev):
     torch.manual_seed(3)
     B, G2, D, n_ctx = 3, 196, 768, 2

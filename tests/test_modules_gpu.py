@@ -152,3 +152,29 @@ def test_module_caption_forward_like_the_reference(dev):
     assert loss.item() == ref.loss()
     for n in ref.trainable_names:
         assert torch.equal(dict(model.named_parameters())[n].grad, ref.G[n]), n
+
+
+def test_image_encoder_with_caption_embeddings(dev):
+    """image_encoder(x, shared_ctx, deep_vis, clip_embeddings) (clip/model.py:509, 550-561): the caption tokens'
+    embedding pooled with a fresh random vector, projected by a fresh random Linear(512, 768), prepended to
+    every deep prompt -- the growing sequence of the engine's caption path, bit for bit with the same draws,
+    and the reference's image features (tests/golden/case_cap_c1_j3_b4.npz) within the fp16 floor."""
+    from federated_multi_modal_amd.captions import caption_tokens, draw_caption_weights
+    c = C.load_case("cap_c1_j3_b4")
+    J, K, B, seed, names, batch = C.case_inputs(c)
+    caps = [str(x) for x in c["captions"]]
+    e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed), device=dev)
+    model = CustomCLIP(e).eval()
+    img = torch.from_numpy(batch.images).to(dev)
+    prompts, shared_ctx, deep_text, deep_vis = model.prompt_learner()
+    tok = torch.from_numpy(caption_tokens(caps)).to(dev)
+    emb = model.clip_model2.token_embedding.weight[tok].half()        # trainers/maple.py:319
+    model.caption_generator = torch.Generator().manual_seed(int(c["cap_seed"]))
+    imf = model.image_encoder(img.half(), shared_ctx, deep_vis, emb)
+    ref = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed, captions=True), device=dev)
+    ref.set_captions(tok.cpu(), draw_caption_weights(torch.Generator().manual_seed(int(c["cap_seed"]))))
+    ref.load_batch(img)
+    ref.forward()
+    assert torch.equal(imf, ref.img_feat)
+    a, b = imf.double().cpu().numpy(), c["img_feat"].astype(np.float64)
+    assert np.linalg.norm(a - b) / np.linalg.norm(b) <= 3e-3

@@ -211,6 +211,19 @@ def test_library_loads_and_exports_every_symbol():
     assert b"multiple of 64" in h.mf_last_error()
 
 
+def test_fused_qkv_attention_shape_rule():
+    """Host side of mf_qkv_attention_fwd: the shapes it covers (the vision blocks, D = 768 at 193..208 tokens;
+    the text blocks, D = 512 causal at 65..80 tokens) and the argument checks that run before any launch."""
+    from federated_multi_modal_amd import _lib, ops
+    assert ops.qkv_attention_supported(32, 199, 12, False) and ops.qkv_attention_supported(38, 77, 8, True)
+    assert not ops.qkv_attention_supported(32, 199, 12, True) and not ops.qkv_attention_supported(38, 10, 8, True)
+    assert not ops.qkv_attention_supported(32, 455, 12, False)  # the caption path's grown sequences
+    h = _lib.lib()
+    assert h.mf_qkv_attention_fwd(None, 768, 10, None, None, None, 2304, None, 768, None, 199, 1, 199, 12, 0,
+                                  None) != 0  # x_rows < N*L: refused on the host
+    assert b"fewer than" in h.mf_last_error()
+
+
 def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
     from federated_multi_modal_amd import _lib
     monkeypatch.setattr(_lib, "_LIB", None)

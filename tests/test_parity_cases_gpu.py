@@ -2,9 +2,11 @@
 
 Each case regenerates the reference's inputs and weights with the portable PRNG and runs the MI355X
 engine (every op a libmapfed.so kernel) on them:
-  * logits: the gate of DESIGN.md §5 (tests/_cases.py logit_gate): max |d| <= 4e-3, mean |d| <= 1.5e-3,
-    distance to the float64 restatement <= 1.25x the reference's own, argmax identical on every row
-    whose top-2 margin exceeds 4e-3 (trainers/maple.py:304-346, :674-677);
+  * logits: the gate of DESIGN.md §5 (tests/_cases.py logit_gate, against the per-fixture fp16 floor of
+    tests/golden/floors.json): max |d| <= max(4e-3, 1.25 x the exact-GEMM reference's), mean likewise,
+    distance to the float64 restatement <= 1.25x the larger of the reference's and the exact-GEMM
+    reference's, argmax identical on every row whose top-2 margin exceeds the max gate
+    (trainers/maple.py:304-346, :674-677);
   * train loss within 2 fp16 ulps (trainers/maple.py:349-378);
   * tower features (image_encoder / text_encoder outputs, clip/model.py:509-572, trainers/maple.py:52-79):
     relative L2 distance to the float64 restatement <= 1.25x the reference's own + 1e-4;
@@ -54,7 +56,7 @@ def test_case_parity(name, dev):
     e.load_batch(torch.from_numpy(batch.images), torch.from_numpy(batch.labels))
     logits = e.forward().float().cpu().numpy()
     rep = {"case": name, "J": J, "K": K, "B": B}
-    ok, rep["logits"] = C.logit_gate(logits, c["logits"], c["logits64"])
+    ok, rep["logits"] = C.logit_gate(logits, c["logits"], c["logits64"], C.case_floor(name))
     print(f"{name}: logits {rep['logits']}")
 
     # tower features against the float64 restatement
@@ -153,8 +155,15 @@ def test_case_parity(name, dev):
                 u = np.exp2(np.floor(np.log2(np.maximum(np.abs(p0), 2.0 ** -14))) - 10)
                 if not (diff <= u + 0.1 * np.abs(ref) + 1e-12).all():
                     grad_bad.append(("delta16/" + n, float((diff / u).max()), 0.0))
-            elif np.linalg.norm(ref) > 0 and _rel(ours, ref) > 5e-2:
-                grad_bad.append(("delta/" + n, _rel(ours, ref), 0.0))
+            elif np.linalg.norm(ref) > 0:
+                # fp32 params: delta = -lr * (clip_coef * g + wd * p), so it inherits the gradient's distance
+                # to the reference, which the gradient gate bounds by (1 + 1.25) x the reference's own fp64
+                # distance (triangle inequality); + 2e-2 for the fp32 rounding of p + delta (deltas here are
+                # >= 80 ulps of p)
+                r64 = next(t["ref_vs64"] for t in table if t["tensor"] == n) if any(
+                    t["tensor"] == n for t in table) else 0.0
+                if _rel(ours, ref) > max(5e-2, 2.25 * r64 + 2e-2):
+                    grad_bad.append(("delta/" + n, _rel(ours, ref), r64))
     _report(name, rep)
     assert ok, rep["logits"]
     assert loss_ok, rep["loss"]
