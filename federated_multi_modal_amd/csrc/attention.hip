@@ -459,10 +459,10 @@ MF_DEV void qkv_dma_issue(const f16* x, int x_bytes, const f16* w, int w_bytes, 
 }
 
 template <int LKP, int MR, int D, bool CAUSAL, int NR>
-__global__ __launch_bounds__(MR / 32 * 2 * 64) void qkv_attn_fwd_kernel(
-    const f16* __restrict__ x, int64_t ld_x, int x_rows, const f16* __restrict__ w, const f16* __restrict__ bias,
-    f16* __restrict__ qkv, int64_t ld_qkv, f16* __restrict__ out, int64_t ld_out, float* __restrict__ lse,
-    int ld_lse, int L, int H) {
+MF_DEV void qkv_attn_fwd_body(const f16* __restrict__ x, int64_t ld_x, int x_rows, const f16* __restrict__ w,
+                              const f16* __restrict__ bias, f16* __restrict__ qkv, int64_t ld_qkv,
+                              f16* __restrict__ out, int64_t ld_out, float* __restrict__ lse, int ld_lse, int L,
+                              int H) {
   constexpr int WMG = MR / 32, NW = 2 * WMG, NT = 64 * NW;
   constexpr int HK = 32, KS = 64, NKT = D / KS;  // k-subs of 32; a K-step (ring slot) holds two
   constexpr int NA = MR / 16, NB = 192 / 16;     // LDS-DMA wave instructions (16 rows x 64 B) per k-sub
@@ -522,13 +522,6 @@ __global__ __launch_bounds__(MR / 32 * 2 * 64) void qkv_attn_fwd_kernel(
                                    (kt) * KS * 2 + HK * 2, wid);                                             \
   } while (0)
 
-  // bias of this lane's output columns (read before the DMA stream, so the first retire covers it)
-  f16x4 bv[6];
-#pragma unroll
-  for (int jj = 0; jj < 6; ++jj) {
-    const int j = 6 * ng + jj;
-    bv[jj] = *(const f16x4*)(bias + (j >> 2) * D + h * 64 + 16 * (j & 3) + 4 * fg);
-  }
   f32x4 acc[2][6];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -562,6 +555,14 @@ __global__ __launch_bounds__(MR / 32 * 2 * 64) void qkv_attn_fwd_kernel(
     }
   }
   MF_ASTAMP2(1);
+  // bias of this lane's output columns, loaded after the K loop (12 VGPRs the loop does not hold: the text
+  // kernel fits 128 VGPRs with it out of the loop); its latency overlaps the barrier
+  f16x4 bv[6];
+#pragma unroll
+  for (int jj = 0; jj < 6; ++jj) {
+    const int j = 6 * ng + jj;
+    bv[jj] = *(const f16x4*)(bias + (j >> 2) * D + h * 64 + 16 * (j & 3) + 4 * fg);
+  }
   __syncthreads();  // every wave is done with the ring
 
   // q / k / v images: fp16(acc + bias) (the GEMM's EPI_BIAS rounding); lane holds row
@@ -609,6 +610,24 @@ __global__ __launch_bounds__(MR / 32 * 2 * 64) void qkv_attn_fwd_kernel(
   }
   MF_ASTAMP2(3);
 }
+
+#define MF_QKV_ARGS                                                                                              \
+  const f16 *__restrict__ x, int64_t ld_x, int x_rows, const f16 *__restrict__ w, const f16 *__restrict__ bias, \
+      f16 *__restrict__ qkv, int64_t ld_qkv, f16 *__restrict__ out, int64_t ld_out, float *__restrict__ lse,    \
+      int ld_lse, int L, int H
+// vision (D = 768, 193..208 rows): 14 waves, the 160 KB ring: one workgroup per CU
+__global__ __launch_bounds__(896) void qkv_attn_fwd_vision_kernel(MF_QKV_ARGS) {
+  qkv_attn_fwd_body<208, 224, 768, false, 3>(x, ld_x, x_rows, w, bias, qkv, ld_qkv, out, ld_out, lse, ld_lse, L, H);
+}
+// text (D = 512, causal, 65..80 rows): 6 waves and 72 KB of LDS, so two workgroups per CU by LDS -- but only
+// if no SIMD needs a 4th wave: waves are dealt to the SIMDs cyclically from a varying start, so the second
+// workgroup's two-wave SIMDs can be the first's.  At 129 VGPRs (3 waves per SIMD) the stamps
+// (tests/diagnostics/qkv_stamps.cpp) showed one workgroup per CU; at <= 128 (4 per SIMD: the bias load out
+// of the K loop, 117 VGPRs) any placement fits.
+__global__ __launch_bounds__(384) void qkv_attn_fwd_text_kernel(MF_QKV_ARGS) {
+  qkv_attn_fwd_body<80, 96, 512, true, 2>(x, ld_x, x_rows, w, bias, qkv, ld_qkv, out, ld_out, lse, ld_lse, L, H);
+}
+#undef MF_QKV_ARGS
 
 // Dq[nh][q] = sum_d dO[q][d] * O[q][d] (fp32) ------------------------------------------------
 __global__ void attn_bwd_dot_kernel(const f16* __restrict__ out, int64_t ld_out, const f16* __restrict__ dout,
@@ -1242,11 +1261,11 @@ extern "C" int mf_qkv_attention_fwd(const void* x, int64_t ld_x, int x_rows, con
   if (x_rows < N * L) return mf_set_error("mf_qkv_attention_fwd: x has fewer than N*L rows", -1);
   hipStream_t st = (hipStream_t)stream;
   if (D == 768 && !causal && L > 192 && L <= 208) {
-    qkv_attn_fwd_kernel<208, 224, 768, false, 3><<<N * H, 896, 0, st>>>(
+    qkv_attn_fwd_vision_kernel<<<N * H, 896, 0, st>>>(
         (const f16*)x, ld_x, x_rows, (const f16*)w, (const f16*)bias, (f16*)qkv, ld_qkv, (f16*)out, ld_out, lse,
         ld_lse, L, H);
   } else if (D == 512 && causal && L > 64 && L <= 80) {
-    qkv_attn_fwd_kernel<80, 96, 512, true, 2><<<N * H, 384, 0, st>>>(
+    qkv_attn_fwd_text_kernel<<<N * H, 384, 0, st>>>(
         (const f16*)x, ld_x, x_rows, (const f16*)w, (const f16*)bias, (f16*)qkv, ld_qkv, (f16*)out, ld_out, lse,
         ld_lse, L, H);
   } else {

@@ -43,8 +43,9 @@ struct GemmArgs {
   int64_t lda, ldb, ldc, ld_aux;
   int M, N, K;
   int vec8;    // C / aux row strides are multiples of 8 elements -> 16-byte epilogue accesses
-  int ksplit;  // > 0: split-K slice of ksplit (multiple of 64) per blockIdx.z, fp32 partial at C + z*M*ldc
-  int xb;      // log2 of the N-range count of the XCD blocking (tile_of); 0: M-ranges only
+  int ksplit;  // > 0: split-K slice of ksplit (multiple of 64) per slice z, fp32 partial at C + z*M*ldc
+  int xb;      // log2 of the N-range count of the XCD blocking (tile_of); 0: M-ranges only; split-K: 1 =
+               // N-major positions inside a slice (split_tile_of)
 };
 
 // The QuickGELU pre-activation (EPI_BIAS_GELU's aux output) is read again only by the backward, so it is
@@ -78,6 +79,24 @@ MF_DEV void tile_of(int p, int tiles_m, int tiles_n, int xb, int& mt, int& nt) {
     off += sz;
   }
   mt = nt = 0;  // unreachable for p < tiles_m * tiles_n
+}
+
+// Split-K position p (0 .. splits*tiles-1): slice-major, so an XCD's contiguous range of positions is a
+// run of one slice's tiles (and at most a piece of the next) and its L2 holds that slice's K-window of the
+// few A and B panels the run touches, instead of every XCD reading every slice's panels (r02 PMC: the
+// block-11 weight gradients read 163 MB per launch against 49 MB of operands with the slice in
+// blockIdx.z).  Inside a slice the run goes along the longer tile dimension (n_major: M inner).
+MF_DEV void split_tile_of(int p, int tiles_m, int tiles_n, bool n_major, int& z, int& mt, int& nt) {
+  const int tiles = tiles_m * tiles_n;
+  z = p / tiles;
+  const int q = p - z * tiles;
+  if (n_major) {
+    nt = q / tiles_m;
+    mt = q - nt * tiles_m;
+  } else {
+    mt = q / tiles_n;
+    nt = q - mt * tiles_n;
+  }
 }
 
 // Elementwise epilogue on 8 consecutive columns (fp16 staged value t = the GEMM result rounded at
@@ -340,13 +359,6 @@ MF_DEV void dma_stage(const f16* A, int a_bytes, const f16* B, int b_bytes, f16*
 template <int BM, int BN, int WM, int WN, int S, int EPI, bool TA = false, bool TB = false>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g0) {
   GemmArgs g = g0;
-  if (g.ksplit > 0) {  // split-K: this workgroup's K slice and partial-sum plane (EPI_F32)
-    const int k0 = blockIdx.z * g.ksplit;
-    g.A += (int64_t)k0 * (TA ? g.lda : 1);
-    g.B += (int64_t)k0 * (TB ? g.ldb : 1);
-    g.K = min(g.ksplit, g.K - k0);
-    g.C = (float*)g.C + (int64_t)blockIdx.z * g.M * g.ldc;
-  }
   constexpr int NW = WM * WN;
   constexpr int NT = NW * 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;  // per-wave tile
@@ -367,12 +379,30 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(GemmArgs g0) {
   // XCD-aware bijective remap (cdna_hip_programming.md §5 'XCD swizzle must be bijective'):
   // consecutive tile ids (same A row panel) land on one XCD's L2
   const int tiles_n = (g.N + BN - 1) / BN;
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
+  const int tiles_m = (g.M + BM - 1) / BM;
+  // split-K with xb = 2: the r02 order (A/B baseline): slice = dispatch id / tiles, remap inside the slice
+  const bool legacy = g.ksplit > 0 && g.xb == 2;
+  const int nwg = legacy ? tiles_m * tiles_n : gridDim.x;
+  const int bid = legacy ? blockIdx.x % nwg : blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   int mt, nt;
-  tile_of(wgid, (g.M + BM - 1) / BM, tiles_n, g.xb, mt, nt);
+  if (g.ksplit > 0) {  // split-K: this workgroup's K slice and partial-sum plane (EPI_F32)
+    int z;
+    if (legacy) {
+      z = blockIdx.x / nwg;
+      tile_of(wgid, tiles_m, tiles_n, 0, mt, nt);
+    } else {
+      split_tile_of(wgid, tiles_m, tiles_n, g.xb != 0, z, mt, nt);
+    }
+    const int k0 = z * g.ksplit;
+    g.A += (int64_t)k0 * (TA ? g.lda : 1);
+    g.B += (int64_t)k0 * (TB ? g.ldb : 1);
+    g.K = min(g.ksplit, g.K - k0);
+    g.C = (float*)g.C + (int64_t)z * g.M * g.ldc;
+  } else {
+    tile_of(wgid, tiles_m, tiles_n, g.xb, mt, nt);
+  }
   const int m0 = mt * BM;
   const int n0 = nt * BN;
 
@@ -819,7 +849,7 @@ template <int BM, int BN, int WM, int WN, int S, bool TA = false, bool TB = fals
 int launch_tile(const GemmArgs& a, int epi, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const int splits = a.ksplit > 0 ? (a.K + a.ksplit - 1) / a.ksplit : 1;
-  dim3 grid(tiles, 1, splits), block(WM * WN * 64);
+  dim3 grid(tiles * splits), block(WM * WN * 64);
   switch (epi) {
     case EPI_NONE: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_NONE, TA, TB><<<grid, block, 0, st>>>(a); break;
     case EPI_BIAS: gemm_nt_kernel<BM, BN, WM, WN, S, EPI_BIAS, TA, TB><<<grid, block, 0, st>>>(a); break;
@@ -1003,7 +1033,15 @@ extern "C" int mf_gemm_splitk(const void* A, int64_t lda, int a_kmajor, const vo
   splits = (K + ks - 1) / ks;
   if ((int64_t)splits * M * N > ws_floats) return mf_set_error("mf_gemm_splitk: workspace too small", -1);
   hipStream_t st = (hipStream_t)stream;
-  GemmArgs a{(const f16*)A, (const f16*)B, ws, nullptr, nullptr, nullptr, lda, ldb, (int64_t)N, 0, M, N, K, 1, ks, 0};
+  // workgroup order: slice-major positions with each slice's run along the longer tile dimension
+  // (split_tile_of) for >= 96 output tiles, else the r02 order (slice = dispatch id / tiles).  Same-box A/B
+  // (tests/diagnostics/splitk_bench.py, profiles/r03_v1_splitk_order_ab.txt, two runs each): slice-major
+  // v.dW_proj 52.1 -> 48.1 us, v.dW_qkv 40.2 -> 38.4, v.dW_fc 51.6 -> 50.1; but v.dW_out (36 tiles x 8)
+  // 25.2 -> 26.9 and t.dW_fc (64 tiles x 4) 22.2 -> 24.1.  MAPFED_SPLITK_ORDER=0 / 1 forces one order.
+  static const int order = getenv("MAPFED_SPLITK_ORDER") ? atoi(getenv("MAPFED_SPLITK_ORDER")) : -1;
+  const bool slice_major = order < 0 ? tiles >= 96 : order != 0;
+  GemmArgs a{(const f16*)A, (const f16*)B, ws, nullptr, nullptr, nullptr, lda, ldb, (int64_t)N, 0, M, N, K, 1, ks,
+             slice_major ? ((N > M) ? 1 : 0) : 2};
   int rc;
   if (a_kmajor && b_kmajor) rc = launch_tile<128, 128, 2, 2, 2, true, true>(a, EPI_F32, st);
   else if (a_kmajor) rc = launch_tile<128, 128, 2, 2, 2, true, false>(a, EPI_F32, st);

@@ -139,6 +139,11 @@ CASES = [
     ("j9_k38_b4", 5, 1, 0, 9, 38, 4, False, False),
     # the bench's own workload (BASELINE configs[3] per client: PatternNet 38 classes, B=32, J=9)
     ("c4_j9_k38_b32", 4, 2, 0, 9, 38, 32, True, True),
+    # more rows at the bench's shape (eval logits, features, loss): 4 x 32 images on other seeds / clients
+    ("c4e_s6_b32", 6, 0, 1, 9, 38, 32, False, False),
+    ("c4e_s7_b32", 7, 1, 2, 9, 38, 32, False, False),
+    ("c4e_s8_b32", 8, 3, 0, 9, 38, 32, False, False),
+    ("c4e_s9_b32", 9, 2, 3, 9, 38, 32, False, False),
     # CLIP byte-level BPE ids (the reference's own SimpleTokenizer over bpe_small_merges.txt.gz) for the
     # ctx init and the class prompts of real PatternNet class names
     ("bpe_j3_k10_b4", 3, 0, 0, 3, 10, 4, True, False, True),
