@@ -501,7 +501,8 @@ def main():
         roof = {"bound": "mfma", "achieved": ps["tflops"], "peak": MFMA_PEAK_F16 / 1e12, "unit": "TFLOP/s",
                 "frac": ps["tflops"] * 1e12 / MFMA_PEAK_F16, "traffic": traffic, "traffic_unit": "bytes/launch",
                 "traffic_source": traffic_src, "algorithmic_bytes_per_launch": ps["bytes_per_launch"],
-                "kernel": "GEMM family: gemm_nt_kernel + gemm8_kernel (every projection GEMM, fwd+bwd)",
+                "kernel": "GEMM family: gemm_nt_kernel + gemm8(s)_kernel + the hipBLASLt-routed plain / bias-only products "
+                          "(vision in-projection, c_fc dX; csrc/blaslt.hip) -- every projection GEMM, fwd+bwd",
                 "launches_per_step": ps["launches"] // 2,
                 "avg_launch_us": ps["avg_us"], "flop_per_launch": ps["flops_per_launch"]}
     else:

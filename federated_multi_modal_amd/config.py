@@ -184,7 +184,12 @@ def extend_cfg(cfg: CfgNode) -> None:
     """train.py:83-138."""
     cfg.TRAINER.COOP = CfgNode(dict(N_CTX=16, CSC=False, CTX_INIT="", PREC="fp16", CLASS_TOKEN_POSITION="end"))
     cfg.TRAINER.COCOOP = CfgNode(dict(N_CTX=16, CTX_INIT="", PREC="fp16"))
-    cfg.TRAINER.MAPLE = CfgNode(dict(N_CTX=2, CTX_INIT="a photo of a", PREC="fp16", PROMPT_DEPTH=9))
+    # EOT_TRUNCATE (MI355X addition, off by default): run the text tower on the first max(EOT) + 1 tokens
+    # only.  The causal mask makes every later position dead for the EOT features, so logits and loss are
+    # bit-identical (tests/test_engine_gpu.py::test_eot_truncated_text_tower_matches_full); gradients agree
+    # up to fp32 summation order (the GEMM tiles follow the smaller row count).
+    cfg.TRAINER.MAPLE = CfgNode(dict(N_CTX=2, CTX_INIT="a photo of a", PREC="fp16", PROMPT_DEPTH=9,
+                                     EOT_TRUNCATE=False))
     cfg.DATASET.SUBSAMPLE_CLASSES = "all"
     cfg.TRAINER.IVLP = CfgNode(dict(N_CTX_VISION=2, N_CTX_TEXT=2, CTX_INIT="a photo of a", PREC="fp16",
                                     PROMPT_DEPTH_VISION=9, PROMPT_DEPTH_TEXT=9))

@@ -934,6 +934,10 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int S, int M,
 
 }  // namespace
 
+extern "C" int mf_gemm_lib_wants(int M, int N, int K, int epilogue);
+extern "C" int mf_gemm_lib(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N,
+                           int K, const void* bias, int epilogue, void* stream);
+
 // C[M,N] = epilogue(op(A) . op(B)^T):  a_kmajor = 0: A[m][k] at A[m*lda + k], 1: A[k*lda + m];
 // b_kmajor = 0: B[n][k] at B[n*ldb + k], 1: B[k*ldb + n].
 extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb, int b_kmajor, void* C,
@@ -963,6 +967,9 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     if (tile == 0) tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
     return launch_kmajor(a, a_kmajor != 0, b_kmajor != 0, epilogue, tile, st);
   }
+  // the plain / bias-only products the vendor library runs faster (blaslt.hip; off until mf_gemm_lib_init)
+  if (tile == 0 && mf_gemm_lib_wants(M, N, K, epilogue))
+    return mf_gemm_lib(A, lda, B, ldb, C, ldc, M, N, K, bias, epilogue, stream);
   if (tile == 0) {  // heuristic: fill the 256 CUs (measured: tests/diagnostics/gemm_bench.py, gemm_stamps.cpp)
     const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
     if (t256 >= 192 && t256 <= 256 && K >= 512)

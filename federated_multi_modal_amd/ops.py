@@ -112,6 +112,29 @@ def _rec(ev):
         ev.record()
 
 
+# hipBLASLt for the plain / bias-only products it runs faster (csrc/blaslt.hip): one workspace per process
+GEMM_LIB_WS_BYTES = 64 << 20
+_LIB_WS: Optional[torch.Tensor] = None
+
+
+def gemm_lib_init(device) -> None:
+    """Create the hipBLASLt handle and hand it a workspace that outlives every captured graph (idempotent);
+    from then on mf_gemm's heuristic tile path routes the products mf_gemm_lib_wants() names to hipBLASLt."""
+    global _LIB_WS
+    if _LIB_WS is None:
+        _LIB_WS = torch.empty(GEMM_LIB_WS_BYTES, dtype=torch.uint8, device=device)
+        call("mf_gemm_lib_init", _p(_LIB_WS), GEMM_LIB_WS_BYTES)
+
+
+def gemm_lib_enable(on: bool) -> None:
+    """Route (True) or keep (False) the library-eligible products off the hand-written kernels."""
+    call("mf_gemm_lib_enable", int(bool(on)))
+
+
+def gemm_lib_wants(M: int, N: int, K: int, epilogue: int) -> bool:
+    return bool(call("mf_gemm_lib_wants", M, N, K, epilogue))
+
+
 def gemm_nt(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NONE, tile=0):
     """C[M,N] = epi(A[M,K] . B[N,K]^T)."""
     M, K = A.shape

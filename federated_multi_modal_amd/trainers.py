@@ -177,7 +177,8 @@ class MaPLe(TrainerX):
         ecfg = EngineConfig(batch=cfg.DATALOADER.TRAIN_X.BATCH_SIZE, classnames=list(classnames),
                             prompt_depth=mcfg.PROMPT_DEPTH, seed=max(cfg.SEED, 0), n_ctx=mcfg.N_CTX,
                             ctx_init=mcfg.CTX_INIT, momentum=cfg.OPTIM.MOMENTUM,
-                            weight_decay=cfg.OPTIM.WEIGHT_DECAY, bpe_path=bpe)
+                            weight_decay=cfg.OPTIM.WEIGHT_DECAY, bpe_path=bpe,
+                            eot_truncate=bool(mcfg.get("EOT_TRUNCATE", False)))
         if dims is not None:
             ecfg.dims = dims
         if cfg.OPTIM.NAME != "sgd":

@@ -20,3 +20,14 @@ def dev():
     if not torch.cuda.is_available():
         pytest.fail("GPU test selected but no GPU is visible")
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def handwritten_gemm(dev):
+    """Keep every product on the hand-written GEMM kernels for the test (the hipBLASLt route of
+    csrc/blaslt.hip off), for tests that compare two hand-written paths bit for bit."""
+    from federated_multi_modal_amd import ops
+    ops.gemm_lib_init(dev)
+    ops.gemm_lib_enable(False)
+    yield
+    ops.gemm_lib_enable(True)

@@ -339,10 +339,10 @@ def test_c5_full_size_properties(dev):
     assert torch.equal(l0, l2) and s0 == s2
 
 
-def test_fused_qkv_attention_does_not_change_results(dev, monkeypatch):
-    """The in-projection + attention forward as one launch (MAPFED_FUSED_QKV_ATTN, on by default for both
-    towers) against the unfused pair: logits, loss and every gradient bit-identical at the c4 client shape
-    (J = 9, K = 38, B = 32)."""
+def test_fused_qkv_attention_does_not_change_results(dev, monkeypatch, handwritten_gemm):
+    """The in-projection + attention forward as one launch (MAPFED_FUSED_QKV_ATTN=1, opt-in) against the
+    unfused pair on the hand-written GEMM: logits, loss and every gradient bit-identical at the c4 client
+    shape (J = 9, K = 38, B = 32)."""
     J, K, B, seed = 9, 38, 32, 2
     names = syn.synthetic_classnames(K, seed)
     b = syn.client_batch(seed, 0, 0, B, K)

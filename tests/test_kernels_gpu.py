@@ -273,7 +273,7 @@ def test_attention_fwd_bwd(dev, N, L, H, causal):
 
 @pytest.mark.parametrize("N,L,H,causal", [(4, 199, 12, False), (32, 199, 12, False), (3, 193, 12, False),
                                           (38, 77, 8, True), (5, 80, 8, True)])
-def test_qkv_attention_fused_matches_unfused(dev, N, L, H, causal):
+def test_qkv_attention_fused_matches_unfused(dev, handwritten_gemm, N, L, H, causal):
     """mf_qkv_attention_fwd (in-projection + attention in one launch) against the two launches it replaces
     (mf_gemm_nt with the bias epilogue, then mf_attention_fwd): qkv, out and lse bit-identical (same MFMA,
     same k order, same fp16 rounding points), incl. the last sequence of the buffer (rows past it read as 0)."""
@@ -656,3 +656,36 @@ def test_layernorm_bwd_inject_equals_bwd_then_inject_bwd(dev, N, L, D, row0):
     fused.finish()
     assert torch.equal(dx1, dx2) and torch.equal(dg1, dg2) and torch.equal(db1, db2)
     torch.testing.assert_close(pg2, pg1, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(6368, 2304, 768, 1), (6368, 768, 3072, 0), (2926, 512, 2048, 0),
+                                       (300, 200, 128, 1), (130, 96, 64, 0)])
+def test_gemm_lib_route(dev, M, N, K, epi):
+    """csrc/blaslt.hip: hipBLASLt for the plain / bias-only products mf_gemm_lib_wants names (the vision
+    in-projection and the c_fc dX products at their c4 shapes; two small shapes for the layout mapping).
+    Against float64 like every GEMM kernel, deterministic, and bit-identical to the hand-written kernel on the
+    same operands (measured on MI355X for every shape here: the route changes no result of the step)."""
+    ops.gemm_lib_init(dev)
+    g = torch.Generator(device="cpu").manual_seed(M + 7 * N + K)
+    A = torch.randn(M, K, generator=g).half().to(dev)
+    B = (torch.randn(N, K, generator=g) * K ** -0.5).half().to(dev)
+    b = (torch.randn(N, generator=g) * 0.1).half().to(dev) if epi == 1 else None
+    C = torch.full((M, N), float("nan"), device=dev, dtype=torch.float16)
+    ops.call("mf_gemm_lib", ops._p(A), ops._ld(A), ops._p(B), ops._ld(B), ops._p(C), ops._ld(C), M, N, K, ops._p(b),
+             epi, ops._s())
+    ref = A.double() @ B.double().t() + (b.double() if b is not None else 0.0)
+    assert_ulps(C, ref, 1.0, 2e-2, "hipBLASLt gemm")
+    C2 = C.clone()
+    ops.call("mf_gemm_lib", ops._p(A), ops._ld(A), ops._p(B), ops._ld(B), ops._p(C2), ops._ld(C2), M, N, K,
+             ops._p(b), epi, ops._s())
+    assert torch.equal(C, C2)  # deterministic
+    ops.gemm_lib_enable(False)
+    try:
+        H = ops.gemm_nt(A, B, bias=b, epilogue=epi)
+    finally:
+        ops.gemm_lib_enable(True)
+    d = int((C.view(torch.int16).int() - H.view(torch.int16).int()).abs().max())
+    print(f"{M}x{N}x{K} epi {epi}: hipBLASLt vs hand-written: bit-identical {torch.equal(C, H)}, max {d} ulp")
+    assert torch.equal(C, H)
+    if M >= 2048:
+        assert ops.gemm_lib_wants(M, N, K, epi)

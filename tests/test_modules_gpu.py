@@ -85,7 +85,9 @@ def test_eval_and_tower_callables(dev):
     # a batch size other than the engine's (the test loader's 100, trainers/maple.py:671): same logits per row
     with torch.no_grad():
         two = model(img[:2])
-    assert torch.equal(two, logits[:2]) or (two.float() - logits[:2].float()).abs().max() <= 2e-3
+    d = float((two.float() - logits[:2].float()).abs().max())
+    print(f"rows 0-1 at batch 2 vs batch {B}: max |d| = {d:.3e}, bit-identical {torch.equal(two, logits[:2])}")
+    assert torch.equal(two, logits[:2]) or d <= 2e-3
 
 
 def test_reference_training_step_through_the_module(dev):

@@ -378,3 +378,22 @@ def test_caption_generator_shared_by_trainer_and_module(dev, tmp_path):
     c.model.train()
     loss_module = float(c.model(batch["img"], batch["label"], batch["caption"]))
     assert abs(loss_module - loss_trainer) <= 1e-6 * max(1.0, abs(loss_trainer))
+
+
+def test_eot_truncate_config_key(dev, tmp_path):
+    """TRAINER.MAPLE.EOT_TRUNCATE (MI355X addition, default off): the client engines run the text tower on
+    the first max(EOT) + 1 tokens, and a training step's logits and loss equal the full 77-token tower's bit
+    for bit (the causal mask makes every later position dead for the EOT features)."""
+    full = build_trainer(small_cfg(tmp_path / "a", clients=1))
+    trunc = build_trainer(small_cfg(tmp_path / "b", clients=1, extra=["TRAINER.MAPLE.EOT_TRUNCATE", True]))
+    ef, et = full.clients[0].engine, trunc.clients[0].engine
+    assert ef.text_len == 77 and et.text_len < 77
+    batch = next(iter(full.clients[0].dm.train_loader))
+    out = []
+    for c in (full.clients[0], trunc.clients[0]):
+        c.engine.clear_halt()
+        c._load(batch["img"], batch["label"], c.engine)
+        c.engine.forward_backward()
+        out.append((c.engine.logits.detach().cpu().clone(), c.engine.loss()))
+    assert torch.equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
