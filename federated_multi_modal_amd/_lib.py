@@ -62,7 +62,7 @@ SIGNATURES = {
     "mf_fedavg_reduce_ordered": [P, I, L, L, P, P],
     "mf_seq_grow": [P, P, P, P, I, I, I, I, I, P],
     "mf_seq_grow_bwd": [P, P, I, I, I, I, I, P],
-    "mf_caption_pool": [P, I, I, P, P, I, P, P],
+    "mf_caption_pool": [P, I, I, P, I, P, I, P, P],
     "mf_nonfinite_flag": [P, L, I, P, P],
     "mf_augment_ws_bytes": [I, I, I, I],
     "mf_augment": [P, L, P, P, P, I, I, I, I, F, F, F, F, F, F, P, I, P, L, P],

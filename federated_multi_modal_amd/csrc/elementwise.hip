@@ -201,16 +201,23 @@ __global__ void seq_grow_bwd_kernel(const f16* __restrict__ ddst, f16* __restric
 //   s[t]   = fp16(emb[t] . w)                                   (torch.matmul, fp32 accumulate)
 //   p      = fp16(softmax(s))                                   (over the T <= 128 tokens, fp32 math)
 //   pooled = fp16(sum_t fp16(emb[t] * p[t]))                    (fp32 accumulate, tokens in order)
-// one wave per token for the scores, one thread per column for the pooled sum.
+// one wave per token for the scores, one thread per column for the pooled sum.  An id outside [0, vocab)
+// reads no table row: its score is NaN, so the caption's pooled row is NaN and the step's loss check fails
+// loudly (the host range-checks ids before the upload; this guards direct device callers).
 __global__ __launch_bounds__(256) void caption_pool_kernel(const int* __restrict__ tok, int T,
-                                                           const float* __restrict__ table, const f16* __restrict__ w,
-                                                           int D, f16* __restrict__ pooled) {
+                                                           const float* __restrict__ table, int vocab,
+                                                           const f16* __restrict__ w, int D, f16* __restrict__ pooled) {
   __shared__ float s_score[128];
   __shared__ float s_p[128];
   const int b = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int* tb = tok + (int64_t)b * T;
   for (int t = wv; t < T; t += 4) {
-    const float* e = table + (int64_t)tb[t] * D;
+    const int id = tb[t];
+    if (id < 0 || id >= vocab) {
+      if (lane == 0) s_score[t] = NAN;
+      continue;
+    }
+    const float* e = table + (int64_t)id * D;
     float s = 0.f;
     for (int d = lane; d < D; d += 64) s += (float)(f16)e[d] * (float)w[d];
     s = wave_sum(s);
@@ -229,7 +236,11 @@ __global__ __launch_bounds__(256) void caption_pool_kernel(const int* __restrict
   __syncthreads();
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
     float acc = 0.f;
-    for (int t = 0; t < T; ++t) acc += r16((float)(f16)table[(int64_t)tb[t] * D + d] * s_p[t]);
+    for (int t = 0; t < T; ++t) {
+      const int id = tb[t];
+      const float e = (id >= 0 && id < vocab) ? (float)(f16)table[(int64_t)id * D + d] : 0.f;
+      acc += r16(e * s_p[t]);
+    }
     pooled[(int64_t)b * D + d] = (f16)acc;
   }
 }
@@ -566,11 +577,12 @@ extern "C" int mf_seq_grow_bwd(const void* ddst, void* dsrc, int N, int Lp, int 
   return 0;
 }
 
-extern "C" int mf_caption_pool(const int* tokens, int B, int T, const float* table, const void* w, int D, void* pooled,
-                               void* stream) {
+extern "C" int mf_caption_pool(const int* tokens, int B, int T, const float* table, int vocab, const void* w, int D,
+                               void* pooled, void* stream) {
   if (B <= 0) return 0;
   if (T <= 0 || T > 128) return mf_set_error("mf_caption_pool: 0 < T <= 128 tokens", -1);
-  caption_pool_kernel<<<B, 256, 0, (hipStream_t)stream>>>(tokens, T, table, (const f16*)w, D, (f16*)pooled);
+  if (vocab <= 0) return mf_set_error("mf_caption_pool: vocab must be positive", -1);
+  caption_pool_kernel<<<B, 256, 0, (hipStream_t)stream>>>(tokens, T, table, vocab, (const f16*)w, D, (f16*)pooled);
   MF_CHECK_LAUNCH();
   return 0;
 }

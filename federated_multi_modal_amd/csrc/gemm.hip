@@ -686,6 +686,7 @@ __global__ __launch_bounds__(512) void gemm8s_kernel(GemmArgs g) {
   static_assert(LDS_ELEMS * 2 <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(1024))) f16 lds[LDS_ELEMS];
 
+  MF_STAMP(0);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -761,6 +762,7 @@ __global__ __launch_bounds__(512) void gemm8s_kernel(GemmArgs g) {
   for (int h = 0; h < E; ++h) issue(h);
   wait_vmcnt<INS * (E - 2)>();
   lds_barrier();
+  MF_STAMP(1);
   if (wm == 1) lds_barrier();  // the stagger
   f16x8 fx[QTM], fy[QTM], fb0[TN], fb1[TN];
 
@@ -807,7 +809,9 @@ __global__ __launch_bounds__(512) void gemm8s_kernel(GemmArgs g) {
   (void)nh;
   if (wm == 0) lds_barrier();  // even out the barrier count
   __syncthreads();
+  MF_STAMP(2);
   epilogue_store<BM, BN, NT, TM, TN, EPI>(g, lds, acc, m0, n0, wm * WTM, wn * WTN, tid, fr, fg);
+  MF_STAMP(3);
 }
 
 int launch_tile8s(const GemmArgs& a, int epi, hipStream_t st) {

@@ -122,33 +122,55 @@ __global__ void loss_kernel(const f16* __restrict__ logits, const f16* __restric
 // d img_n[b,:] = fp16( fp16(sum_k dmm[b,k] txt_n[k,:]) + cos-path ) ; block per row b
 // cos path (fp32): g_u = dcos*v, d img_n += g_u/nu - img_n*(g_u . img_n)/nu^3 with dcos = fp16(-0.5/B)
 // soft_rows != null: the cosine target of row b is soft_rows[b,:] ((q @ txt_n)[b]) instead of txt_n[y_b]
-__global__ void dimg_kernel(const f16* __restrict__ dmm, const f16* __restrict__ img_n, const f16* __restrict__ txt_n,
-                            const int64_t* __restrict__ label, const f16* __restrict__ soft_rows,
-                            const float* __restrict__ cos_norms, int B, int K, int D, f16* __restrict__ dimg_n) {
-  const int b = blockIdx.x;
+// One wave per (row b, 64-column chunk): grid (B, ceil(D/64)).  The K-long sum of a column runs in k order
+// in one lane (as before), with its loads issued 16 ahead of the FMA chain; g_u . img_n keeps the reduction
+// order of the former 256-thread block (virtual thread t = lane + 64 w sums d = t, t + 256, ..; the four
+// virtual waves' wave_sums added in order), so the result is bit-identical to the one-block-per-row form
+// (which ran 32 blocks and took 342 us at K = 1 000).
+__global__ __launch_bounds__(64) void dimg_kernel(const f16* __restrict__ dmm, const f16* __restrict__ img_n,
+                                                  const f16* __restrict__ txt_n, const int64_t* __restrict__ label,
+                                                  const f16* __restrict__ soft_rows,
+                                                  const float* __restrict__ cos_norms, int B, int K, int D,
+                                                  f16* __restrict__ dimg_n) {
+  const int b = blockIdx.x, lane = threadIdx.x;
   const int y_raw = soft_rows ? 0 : (int)label[b];
   const f16* trow = soft_rows ? soft_rows + (int64_t)b * D : txt_n + (int64_t)((y_raw < 0 || y_raw >= K) ? 0 : y_raw) * D;
   const float dcos = r16(-0.5f / (float)B);
   const float nu = cos_norms[2 * b], nv = cos_norms[2 * b + 1];
-  __shared__ float red[4];
+  const f16* irow = img_n + (int64_t)b * D;
   // g_u . img_n
   float dotp = 0.f;
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    float v = r16((float)trow[d] / nv);
-    dotp += dcos * v * (float)img_n[(int64_t)b * D + d];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    float part = 0.f;
+    for (int d = lane + 64 * w; d < D; d += 256) {
+      float v = r16((float)trow[d] / nv);
+      part += dcos * v * (float)irow[d];
+    }
+    dotp += wave_sum(part);  // ((w0 + w1) + w2) + w3 from 0.f: the former red[0] + red[1] + red[2] + red[3]
   }
-  dotp = wave_sum(dotp);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dotp;
-  __syncthreads();
-  dotp = red[0] + red[1] + red[2] + red[3];
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < K; ++k) s += (float)dmm[(int64_t)b * K + k] * (float)txt_n[(int64_t)k * D + d];
-    const float v = r16((float)trow[d] / nv);
-    const float a = (float)img_n[(int64_t)b * D + d];
-    const float cosg = dcos * v / nu - a * dotp / (nu * nu * nu);
-    dimg_n[(int64_t)b * D + d] = (f16)(r16(s) + r16(cosg));
+  const int d = blockIdx.y * 64 + lane;
+  if (d >= D) return;
+  const f16* dm = dmm + (int64_t)b * K;
+  const f16* tc = txt_n + d;
+  constexpr int U = 16;
+  float s = 0.f;
+  int k = 0;
+  for (; k + U <= K; k += U) {
+    float tv[U], mv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      tv[u] = (float)tc[(int64_t)(k + u) * D];
+      mv[u] = (float)dm[k + u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) s += mv[u] * tv[u];
   }
+  for (; k < K; ++k) s += (float)dm[k] * (float)tc[(int64_t)k * D];
+  const float v = r16((float)trow[d] / nv);
+  const float a = (float)irow[d];
+  const float cosg = dcos * v / nu - a * dotp / (nu * nu * nu);
+  dimg_n[(int64_t)b * D + d] = (f16)(r16(s) + r16(cosg));
 }
 
 // d txt_n[k,:] = fp16( fp16(sum_b dmm[b,k] img_n[b,:]) + sum_{b: y_b = k} cos-path ) ; block per k
@@ -407,7 +429,7 @@ extern "C" int mf_clip_loss_fwd_bwd(const void* img, const void* txt, const void
   hipStream_t st = (hipStream_t)stream;
   loss_kernel<<<1, 1024, 0, st>>>((const f16*)logits, (const f16*)img_n, (const f16*)txt_n, label, B, K, D,
                                  logit_scale, (f16*)dmm, cos_ws, loss_out);
-  dimg_kernel<<<B, 256, 0, st>>>((const f16*)dmm, (const f16*)img_n, (const f16*)txt_n, label, nullptr, cos_ws, B,
+  dimg_kernel<<<dim3(B, (D + 63) / 64), 64, 0, st>>>((const f16*)dmm, (const f16*)img_n, (const f16*)txt_n, label, nullptr, cos_ws, B,
                                  K, D, (f16*)dimg_n);
   dtxt_kernel<<<K, 256, 0, st>>>((const f16*)dmm, (const f16*)img_n, (const f16*)txt_n, label, cos_ws, B, K, D,
                                  (f16*)dtxt_n);
@@ -430,7 +452,7 @@ extern "C" int mf_clip_loss_soft_fwd_bwd(const void* img, const void* txt, const
   soft_target_kernel<<<B, 256, 0, st>>>(label_probs, (const f16*)txt_n, K, D, tgt);
   loss_soft_kernel<<<1, 1024, 0, st>>>((const f16*)logits, (const f16*)img_n, tgt, label_probs, B, K, D, logit_scale,
                                       (f16*)dmm, gtgt, cos_ws, loss_out);
-  dimg_kernel<<<B, 256, 0, st>>>((const f16*)dmm, (const f16*)img_n, (const f16*)txt_n, nullptr, tgt, cos_ws, B, K, D,
+  dimg_kernel<<<dim3(B, (D + 63) / 64), 64, 0, st>>>((const f16*)dmm, (const f16*)img_n, (const f16*)txt_n, nullptr, tgt, cos_ws, B, K, D,
                                  (f16*)dimg_n);
   dtxt_soft_kernel<<<K, 256, 0, st>>>((const f16*)dmm, (const f16*)img_n, label_probs, gtgt, B, K, D,
                                       (f16*)dtxt_n);

@@ -431,7 +431,7 @@ def caption_pool(tokens, table, w, pooled):
     """tokens int32 [B, T] on the device, table fp32 [vocab, D], w fp16 [D] -> pooled fp16 [B, D]."""
     B, T = tokens.shape
     assert tokens.dtype == torch.int32 and table.dtype == torch.float32 and w.dtype == torch.float16
-    call("mf_caption_pool", _p(tokens), B, T, _p(table), _p(w), table.shape[1], _p(pooled), _s())
+    call("mf_caption_pool", _p(tokens), B, T, _p(table), table.shape[0], _p(w), table.shape[1], _p(pooled), _s())
     return pooled
 
 

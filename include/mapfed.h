@@ -146,9 +146,10 @@ int mf_seq_grow(const void* src, void* dst, const void* cap, const float* prompt
 /* previous prompt rows                                                                                     */
 int mf_seq_grow_bwd(const void* ddst, void* dsrc, int N, int Lp, int ncap, int n_ctx, int D, void* stream);
 /* AttentionPooling (clip/model.py:464-476) of B captions from their token ids [B, T] (int32), the fp32     */
-/* token-embedding table and the fp16 weight vector w [D]: pooled [B, D] fp16                                */
-int mf_caption_pool(const int* tokens, int B, int T, const float* table, const void* w, int D, void* pooled,
-                    void* stream);
+/* token-embedding table [vocab, D] and the fp16 weight vector w [D]: pooled [B, D] fp16.  An id outside    */
+/* [0, vocab) reads nothing and makes its caption's pooled row NaN (the step's loss check then raises)      */
+int mf_caption_pool(const int* tokens, int B, int T, const float* table, int vocab, const void* w, int D,
+                    void* pooled, void* stream);
 int mf_transpose_f16(const void* in, int64_t ld_in, void* out, int64_t ld_out, int R, int C, void* stream);
 int mf_colsum_blocks(int R);
 /* out[c] = sum_r in[r,c]; workspace: mf_colsum_blocks(R) * C floats                               */

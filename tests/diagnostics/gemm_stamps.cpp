@@ -7,6 +7,7 @@
 #define MF_GEMM_STAMPS 1
 #include "../../federated_multi_modal_amd/csrc/common.hip"
 #include "../../federated_multi_modal_amd/csrc/gemm.hip"
+#include "../../federated_multi_modal_amd/csrc/blaslt.hip"
 
 #include <algorithm>
 #include <cstdio>
