@@ -20,7 +20,8 @@ int main(int argc, char** argv) {
   int BM = 128, BN = 128;
   if (tile == 2) BN = 64;
   if (tile == 3) BM = BN = 64;
-  if (tile >= 20) { BM = tile == 23 || tile == 24 ? 128 : 256; BN = (tile == 20 || tile == 23) ? 256 : 128; }
+  if (tile >= 20) { BM = tile == 23 || tile == 24 ? 128 : 256; BN = (tile == 20 || tile == 23 || tile >= 27) ? 256 : 128; }
+  // tile 27 (persistent): one stamp row per TILE (start = its loop iteration), not per workgroup
   if (tile == 10) { BM = 160; BN = 128; }
   if (tile == 15) { BM = 96; BN = 128; }
   if (tile == 16) { BM = 160; BN = 64; }

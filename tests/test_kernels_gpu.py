@@ -42,6 +42,30 @@ def test_gemm8_staggered_matches_unstaggered(dev, M, N, K):
     assert torch.equal(C20, C22)
 
 
+@pytest.mark.parametrize("M,N,K", [(33000, 1024, 192), (77000, 2048, 512), (20001, 512, 128), (30000, 760, 128)])
+def test_gemm8_persistent_matches_staggered(dev, M, N, K):
+    """The persistent 256x256 kernel (tile 27: every workgroup walks several tiles, the next tile's first
+    K-steps land under the register-direct epilogue) against gemm8s (tile 20): bit-identical for every fp16
+    epilogue, ragged M included."""
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    A = torch.randn(M, K, generator=g).half().to(dev)
+    B = (torch.randn(N, K, generator=g) * K ** -0.5).half().to(dev)
+    b = (torch.randn(N, generator=g) * 0.1).half().to(dev)
+    R = torch.randn(M, N, generator=g).half().to(dev)
+    for epi in (ops.EPI_NONE, ops.EPI_BIAS, ops.EPI_BIAS_RESID, ops.EPI_BIAS_GELU, ops.EPI_DGELU, ops.EPI_RESID):
+        kw = {"bias": b} if epi in (ops.EPI_BIAS, ops.EPI_BIAS_RESID, ops.EPI_BIAS_GELU) else {}
+        outs = []
+        for tile in (20, 27):
+            aux_out = torch.empty(M, N, device=dev, dtype=torch.float16) if epi == ops.EPI_BIAS_GELU else None
+            aux_in = R if epi in (ops.EPI_BIAS_RESID, ops.EPI_DGELU, ops.EPI_RESID) else None
+            C = ops.gemm_nt(A, B, aux_in=aux_in, aux_out=aux_out, epilogue=epi, tile=tile, **kw)
+            outs.append((C, aux_out))
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0][0], outs[1][0]), f"epilogue {epi}"
+        if epi == ops.EPI_BIAS_GELU:
+            assert torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("M,N,K,tile", [(796, 2304, 768, 0), (6368, 768, 3072, 0), (770, 512, 2048, 1),
                                         (130, 44, 64, 3), (257, 1536, 512, 2), (6368, 3072, 768, 0),
                                         # 8-wave phase-pipelined family (tiles 20 = staggered 256x256, 21,
