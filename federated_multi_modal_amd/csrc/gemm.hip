@@ -1176,6 +1176,19 @@ inline int gemm_rule() {
   return r;
 }
 
+// The text tower (c4: M = 38 x 77 = 2 926 rows) runs on the side stream beside the vision tower, which sets
+// the step; the text tower's own latency has slack (alone 2.46 ms against the vision tower's 4.80 ms,
+// tests/diagnostics/tower_bound_probe.py), but its kernels' CU time is taken from the vision kernels
+// (the step is 5.73 ms, not 4.80).  So its products want the tile that does the most work per CU-second,
+// not the lowest latency: every row-major text product on 160x128 (76..304 workgroups) instead of
+// 96x64 / 96x128 and the hipBLASLt 64x96 tiles (248..744 workgroups): c4 step +2.9 % (same-box A/B, two
+// rounds: 5 585 / 5 617 -> 5 770 / 5 758 img/s; profiles/r03_v7_text_tile_ab.txt).  MAPFED_TEXT_TILE=<id>
+// forces another tile, -1 restores the latency picks (A/B knob).
+inline int text_tile() {
+  static const int t = getenv("MAPFED_TEXT_TILE") ? atoi(getenv("MAPFED_TEXT_TILE")) : 10;
+  return t;
+}
+
 // XCD blocking (tile_of): the N-range count 2^xb minimising one XCD's operand footprint A/(8/2^xb) +
 // B/2^xb (bytes of the A rows and B rows it reads); MAPFED_GEMM_XB overrides (A/B knob, -1 = auto)
 inline int gemm_xcd_split(int M, int N, int K) {
@@ -1256,7 +1269,8 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     return launch_kmajor(a, a_kmajor != 0, b_kmajor != 0, epilogue, tile, st);
   }
   // the plain / bias-only products the vendor library runs faster (blaslt.hip; off until mf_gemm_lib_init)
-  if (tile == 0 && mf_gemm_lib_wants(M, N, K, epilogue))
+  const bool text_rows = M >= 2048 && M < 4096;  // the c4 text tower: its own tile rule (text_tile)
+  if (tile == 0 && !(text_rows && text_tile() > 0) && mf_gemm_lib_wants(M, N, K, epilogue))
     return mf_gemm_lib(A, lda, B, ldb, C, ldc, M, N, K, bias, epilogue, stream);
   if (tile == 0) {  // heuristic: fill the 256 CUs (measured: tests/diagnostics/gemm_bench.py, gemm_stamps.cpp)
     const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
@@ -1270,6 +1284,8 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
       // N = 3072: 160x128 (960 tiles); N = 768: 96x128 (402 tiles, two workgroups per CU) for K >= 2048,
       // 160x64 (480 tiles) for K = 768; +6..37 % over the 128-row tiles
       tile = (N > 1024 || gemm_rule() == 1) ? 10 : (K >= 2048 ? 15 : 16);
+    else if (text_rows && text_tile() > 0)
+      tile = text_tile();
     else if (M >= 2048 && N >= 1024 && K <= 768 && gemm_rule() != 1)
       tile = N >= 2048 ? 15 : 26;  // text (M = 2926): c_fc and its dX on 96x128, QKV on 96x64
     else if (M >= 2048 && N <= 768 && K >= 512 && gemm_rule() != 1 && gemm_rule() != 2)
