@@ -1075,7 +1075,9 @@ inline int attn_threads(int L) {
 // 2 at N*H = 384, 4 at N*H = 48; tests/diagnostics/attn_bench.py), at the cost of re-staging K/V
 inline int attn_qsplit(int NH, int L) {
   static const int qs = getenv("MAPFED_ATTN_QSPLIT") ? atoi(getenv("MAPFED_ATTN_QSPLIT")) : 0;  // tuning knob
-  const int want = qs > 0 ? qs : std::min(4, (768 + NH - 1) / NH);
+  // the text tower's short sequences (L <= 128) alone: MAPFED_ATTN_QSPLIT_TEXT (A/B knob)
+  static const int qst = getenv("MAPFED_ATTN_QSPLIT_TEXT") ? atoi(getenv("MAPFED_ATTN_QSPLIT_TEXT")) : 0;
+  const int want = (L <= 128 && qst > 0) ? qst : qs > 0 ? qs : std::min(4, (768 + NH - 1) / NH);
   return std::max(1, std::min(want, (L + 15) / 16 / 2));
 }
 

@@ -179,7 +179,7 @@ MF_DEV float half_sum(float v) {
   return v;
 }
 
-template <int D>
+template <int D, int RPH = 1>
 __global__ __launch_bounds__(256) void ln_fwd2_kernel(const f16* __restrict__ x, int64_t ldx,
                                                      const int* __restrict__ ridx, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, f16* __restrict__ y,
@@ -187,76 +187,89 @@ __global__ __launch_bounds__(256) void ln_fwd2_kernel(const f16* __restrict__ x,
                                                      float* __restrict__ rstd_out, int rows,
                                                      const float* __restrict__ inj = nullptr, int inj_L = 1,
                                                      int inj_row0 = 0, int inj_n = 0) {
+  // RPH rows per half-wave (consecutive rows, every row's loads issued before the first is reduced): the
+  // same per-row arithmetic with 1/RPH of the workgroups -- for the text tower, whose LayerNorms run beside
+  // the vision tower and should hold as few CUs as possible (no injection: RPH = 1 there)
+  static_assert(RPH == 1 || RPH == 2 || RPH == 4, "rows per half-wave");
   constexpr int CH = D / 256;  // 16-byte chunks per lane
   const int hl = threadIdx.x & 31;
-  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
-  if (row >= rows) return;  // whole half-waves leave together: the butterflies stay within a half
-  const int src = ridx ? ridx[row] : row;
-  const f16* xr = x + (int64_t)src * ldx;
-  float v[CH * 8];
-  f16x8 t[CH];
-  // deep-prompt injection fused in (inj != null, no ridx): rows inj_row0 .. inj_row0+inj_n-1 of every
-  // inj_L-row sequence take fp16(prompt row) -- written back to x as mf_prompt_inject_fwd would -- and
-  // are normalised from those values
-  const int pr = inj ? row % inj_L - inj_row0 : -1;
-  if (pr >= 0 && pr < inj_n) {
-    const float* prow = inj + (int64_t)pr * D;
+  const int row0 = (blockIdx.x * 8 + (threadIdx.x >> 5)) * RPH;
+  if (row0 >= rows) return;  // whole half-waves leave together: the butterflies stay within a half
+  f16x8 t[RPH][CH];
+#pragma unroll
+  for (int r = 0; r < RPH; ++r) {
+    const int row = row0 + r < rows ? row0 + r : row0;  // a past-the-end row re-reads row0, stores nothing
+    const int src = ridx ? ridx[row] : row;
+    const f16* xr = x + (int64_t)src * ldx;
+    // deep-prompt injection fused in (inj != null, no ridx): rows inj_row0 .. inj_row0+inj_n-1 of every
+    // inj_L-row sequence take fp16(prompt row) -- written back to x as mf_prompt_inject_fwd would -- and
+    // are normalised from those values
+    const int pr = inj ? row % inj_L - inj_row0 : -1;
+    if (pr >= 0 && pr < inj_n) {
+      const float* prow = inj + (int64_t)pr * D;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const int c = 8 * (hl + 32 * j);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t[r][j][e] = (f16)prow[c + e];
+        *(f16x8*)(const_cast<f16*>(xr) + c) = t[r][j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < CH; ++j) t[r][j] = *(const f16x8*)(xr + 8 * (hl + 32 * j));
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPH; ++r) {
+    const int row = row0 + r;
+    if (row >= rows) break;
+    float v[CH * 8];
+    // Reduction order identical to ln_fwd_kernel's: a 16-byte chunk holds the 4-element groups of two
+    // of its lanes (2*hl and 2*hl+1); keep them as two partials, butterfly each over the half-wave
+    // (= that kernel's xor 32..2 steps) and add them last (= its xor-1 step).
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[j * 8 + e] = (float)t[r][j][e];
+        if (e < 4) s0 += v[j * 8 + e];
+        else s1 += v[j * 8 + e];
+      }
+    const float mean = (half_sum(s0) + half_sum(s1)) / (float)D;
+    float ss0 = 0.f, ss1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = v[j * 8 + e] - mean;
+        if (e < 4) ss0 += d * d;
+        else ss1 += d * d;
+      }
+    const float var = (half_sum(ss0) + half_sum(ss1)) / (float)D;
+    const float rstd = 1.0f / sqrtf(fmaxf(var, 0.f) + 1e-5f);
+    const float bias = -rstd * mean;
+    f16* yr = y + (int64_t)row * ldy;
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
       const int c = 8 * (hl + 32 * j);
+      const f32x4 g0 = *(const f32x4*)(gamma + c), g1 = *(const f32x4*)(gamma + c + 4);
+      const f32x4 b0 = *(const f32x4*)(beta + c), b1 = *(const f32x4*)(beta + c + 4);
+      f16x8 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) t[j][e] = (f16)prow[c + e];
-      *(f16x8*)(const_cast<f16*>(xr) + c) = t[j];
+      for (int e = 0; e < 8; ++e) {
+        float tt = v[j * 8 + e] * rstd;
+        tt = tt + bias;
+        tt = tt * (e < 4 ? g0[e] : g1[e - 4]);
+        tt = tt + (e < 4 ? b0[e] : b1[e - 4]);
+        o[e] = (f16)tt;
+      }
+      *(f16x8*)(yr + c) = o;
     }
-  } else {
-#pragma unroll
-    for (int j = 0; j < CH; ++j) t[j] = *(const f16x8*)(xr + 8 * (hl + 32 * j));
-  }
-  // Reduction order identical to ln_fwd_kernel's: a 16-byte chunk holds the 4-element groups of two
-  // of its lanes (2*hl and 2*hl+1); keep them as two partials, butterfly each over the half-wave
-  // (= that kernel's xor 32..2 steps) and add them last (= its xor-1 step).
-  float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-  for (int j = 0; j < CH; ++j)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      v[j * 8 + e] = (float)t[j][e];
-      if (e < 4) s0 += v[j * 8 + e];
-      else s1 += v[j * 8 + e];
+    if (hl == 0) {
+      if (mean_out) mean_out[row] = mean;
+      if (rstd_out) rstd_out[row] = rstd;
     }
-  const float mean = (half_sum(s0) + half_sum(s1)) / (float)D;
-  float ss0 = 0.f, ss1 = 0.f;
-#pragma unroll
-  for (int j = 0; j < CH; ++j)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float d = v[j * 8 + e] - mean;
-      if (e < 4) ss0 += d * d;
-      else ss1 += d * d;
-    }
-  const float var = (half_sum(ss0) + half_sum(ss1)) / (float)D;
-  const float rstd = 1.0f / sqrtf(fmaxf(var, 0.f) + 1e-5f);
-  const float bias = -rstd * mean;
-  f16* yr = y + (int64_t)row * ldy;
-#pragma unroll
-  for (int j = 0; j < CH; ++j) {
-    const int c = 8 * (hl + 32 * j);
-    const f32x4 g0 = *(const f32x4*)(gamma + c), g1 = *(const f32x4*)(gamma + c + 4);
-    const f32x4 b0 = *(const f32x4*)(beta + c), b1 = *(const f32x4*)(beta + c + 4);
-    f16x8 o;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float tt = v[j * 8 + e] * rstd;
-      tt = tt + bias;
-      tt = tt * (e < 4 ? g0[e] : g1[e - 4]);
-      tt = tt + (e < 4 ? b0[e] : b1[e - 4]);
-      o[e] = (f16)tt;
-    }
-    *(f16x8*)(yr + c) = o;
-  }
-  if (hl == 0) {
-    if (mean_out) mean_out[row] = mean;
-    if (rstd_out) rstd_out[row] = rstd;
   }
 }
 
@@ -382,6 +395,13 @@ __global__ __launch_bounds__(256) void ln_bwd2_kernel(const f16* __restrict__ dy
 }
 
 // A/B knob: MAPFED_LN=1 selects the wave-per-row kernels
+
+// rows per half-wave of the D = 512 (text) LayerNorm forward (MAPFED_LN_TEXT_RPH, A/B knob)
+inline int ln_text_rph() {
+  static const int r = getenv("MAPFED_LN_TEXT_RPH") ? atoi(getenv("MAPFED_LN_TEXT_RPH")) : 1;
+  return r == 2 || r == 4 ? r : 1;
+}
+
 inline int ln_variant() {
   static const int v = getenv("MAPFED_LN") ? atoi(getenv("MAPFED_LN")) : 2;
   return v;
@@ -397,8 +417,14 @@ extern "C" int mf_layernorm_fwd(const void* x, int64_t ldx, const int* row_index
   const bool v16 = ((uintptr_t)x % 16 == 0) && ((uintptr_t)y % 16 == 0) && (ldx % 8 == 0) && (ldy % 8 == 0);
   if (ln_variant() == 2 && v16 && (D == 768 || D == 512)) {
     const dim3 g2((rows + 7) / 8);
+    const int rph = D == 512 ? ln_text_rph() : 1;
+    const dim3 gr((rows + 8 * rph - 1) / (8 * rph));
     if (D == 768)
       ln_fwd2_kernel<768><<<g2, 256, 0, st>>>((const f16*)x, ldx, row_index, gamma, beta, (f16*)y, ldy, mean, rstd, rows);
+    else if (rph == 2)
+      ln_fwd2_kernel<512, 2><<<gr, 256, 0, st>>>((const f16*)x, ldx, row_index, gamma, beta, (f16*)y, ldy, mean, rstd, rows);
+    else if (rph == 4)
+      ln_fwd2_kernel<512, 4><<<gr, 256, 0, st>>>((const f16*)x, ldx, row_index, gamma, beta, (f16*)y, ldy, mean, rstd, rows);
     else
       ln_fwd2_kernel<512><<<g2, 256, 0, st>>>((const f16*)x, ldx, row_index, gamma, beta, (f16*)y, ldy, mean, rstd, rows);
     MF_CHECK_LAUNCH();
@@ -515,9 +541,17 @@ extern "C" int mf_layernorm_fwd_inject(void* x, int64_t ldx, const float* gamma,
     return rc ? rc : mf_layernorm_fwd(x, ldx, nullptr, gamma, beta, y, ldy, mean, rstd, rows, D, stream);
   }
   const dim3 g2((rows + 7) / 8);
+  const int rph = D == 512 ? ln_text_rph() : 1;
+  const dim3 gr((rows + 8 * rph - 1) / (8 * rph));
   if (D == 768)
     ln_fwd2_kernel<768><<<g2, 256, 0, st>>>((const f16*)x, ldx, nullptr, gamma, beta, (f16*)y, ldy, mean, rstd, rows,
                                             prompt, L, row0, nrows);
+  else if (rph == 2)
+    ln_fwd2_kernel<512, 2><<<gr, 256, 0, st>>>((const f16*)x, ldx, nullptr, gamma, beta, (f16*)y, ldy, mean, rstd,
+                                               rows, prompt, L, row0, nrows);
+  else if (rph == 4)
+    ln_fwd2_kernel<512, 4><<<gr, 256, 0, st>>>((const f16*)x, ldx, nullptr, gamma, beta, (f16*)y, ldy, mean, rstd,
+                                               rows, prompt, L, row0, nrows);
   else
     ln_fwd2_kernel<512><<<g2, 256, 0, st>>>((const f16*)x, ldx, nullptr, gamma, beta, (f16*)y, ldy, mean, rstd, rows,
                                             prompt, L, row0, nrows);
