@@ -505,6 +505,19 @@ def main():
                           "(vision in-projection, c_fc dX; csrc/blaslt.hip) -- every projection GEMM, fwd+bwd",
                 "launches_per_step": ps["launches"] // 2,
                 "avg_launch_us": ps["avg_us"], "flop_per_launch": ps["flops_per_launch"]}
+        by_tower = {}
+        for tower in ("vision", "text"):
+            try:
+                pt = probe.summary(f"gemm/{tower}")
+            except (KeyError, ZeroDivisionError):
+                continue
+            by_tower[tower] = {"launches_per_step": pt["launches"] // 2, "avg_launch_us": pt["avg_us"],
+                               "tflops": pt["tflops"], "frac": pt["tflops"] * 1e12 / MFMA_PEAK_F16,
+                               "flop_per_launch": pt["flops_per_launch"]}
+        roof["by_tower"] = by_tower or None
+        roof["by_tower_note"] = ("the text tower's products run on 160x128 tiles chosen for work per CU-second beside "
+                                 "the vision tower, not for their own latency (DESIGN.md §4): isolated here (towers "
+                                 "serialised) they take longer than the latency picks while the step gets faster")
     else:
         roof = {"bound": "mfma", "achieved": ps["tflops"], "peak": MFMA_PEAK_F16 / 1e12, "unit": "TFLOP/s",
                 "frac": ps["tflops"] * 1e12 / MFMA_PEAK_F16, "traffic": None, "kernel": "attention_fwd_kernel",
