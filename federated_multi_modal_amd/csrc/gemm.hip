@@ -1176,14 +1176,15 @@ inline int gemm_rule() {
   return r;
 }
 
-// The text tower (c4: M = 38 x 77 = 2 926 rows) runs on the side stream beside the vision tower, which sets
-// the step; the text tower's own latency has slack (alone 2.46 ms against the vision tower's 4.80 ms,
-// tests/diagnostics/tower_bound_probe.py), but its kernels' CU time is taken from the vision kernels
-// (the step is 5.73 ms, not 4.80).  So its products want the tile that does the most work per CU-second,
-// not the lowest latency: every row-major text product on 160x128 (76..304 workgroups) instead of
-// 96x64 / 96x128 and the hipBLASLt 64x96 tiles (248..744 workgroups): c4 step +2.9 % (same-box A/B, two
-// rounds: 5 585 / 5 617 -> 5 770 / 5 758 img/s; profiles/r03_v7_text_tile_ab.txt).  MAPFED_TEXT_TILE=<id>
-// forces another tile, -1 restores the latency picks (A/B knob).
+// Tile -1 = "off the critical path": the products of the tower that runs beside the one setting the step
+// (the engine passes it: the text tower at c4, the vision tower at C5).  That tower's own latency has slack
+// (c4: text alone 2.46 ms against the vision tower's 4.80 ms, tests/diagnostics/tower_bound_probe.py), but its
+// kernels' CU time is taken from the critical tower's kernels (the c4 step is 5.73 ms, not 4.80).  So its
+// products want the tile that does the most work per CU-second, not the lowest latency: 160x128 for every
+// row-major product of >= 2 048 rows (c4 text: 76..304 workgroups instead of the latency picks' 96x64 / 96x128
+// and hipBLASLt's 64x96, 248..744 workgroups): c4 step +2.9 % (same-box A/B, two rounds: 5 585 / 5 617 ->
+// 5 770 / 5 758 img/s; profiles/r03_v7_text_tile_ab.txt); C5 vision +0.6..0.8 %.  MAPFED_TEXT_TILE=<id> forces
+// another tile for them, -1 the latency picks (A/B knob).
 inline int text_tile() {
   static const int t = getenv("MAPFED_TEXT_TILE") ? atoi(getenv("MAPFED_TEXT_TILE")) : 10;
   return t;
@@ -1265,12 +1266,14 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
   hipStream_t st = (hipStream_t)stream;
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   if (a_kmajor || b_kmajor) {
-    if (tile == 0) tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
+    if (tile <= 0) tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
     return launch_kmajor(a, a_kmajor != 0, b_kmajor != 0, epilogue, tile, st);
   }
   // the plain / bias-only products the vendor library runs faster (blaslt.hip; off until mf_gemm_lib_init)
-  const bool text_rows = M >= 2048 && M < 4096;  // the c4 text tower: its own tile rule (text_tile)
-  if (tile == 0 && !(text_rows && text_tile() > 0) && mf_gemm_lib_wants(M, N, K, epilogue))
+  // tile -1: a product of the tower off the step's critical path (throughput tiles, see text_tile)
+  const bool side = tile == -1 && M >= 2048 && text_tile() > 0;
+  if (tile == -1) tile = side ? text_tile() : 0;
+  if (tile == 0 && mf_gemm_lib_wants(M, N, K, epilogue))
     return mf_gemm_lib(A, lda, B, ldb, C, ldc, M, N, K, bias, epilogue, stream);
   if (tile == 0) {  // heuristic: fill the 256 CUs (measured: tests/diagnostics/gemm_bench.py, gemm_stamps.cpp)
     const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
@@ -1284,8 +1287,6 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
       // N = 3072: 160x128 (960 tiles); N = 768: 96x128 (402 tiles, two workgroups per CU) for K >= 2048,
       // 160x64 (480 tiles) for K = 768; +6..37 % over the 128-row tiles
       tile = (N > 1024 || gemm_rule() == 1) ? 10 : (K >= 2048 ? 15 : 16);
-    else if (text_rows && text_tile() > 0)
-      tile = text_tile();
     else if (M >= 2048 && N >= 1024 && K <= 768 && gemm_rule() != 1)
       tile = N >= 2048 ? 15 : 26;  // text (M = 2926): c_fc and its dX on 96x128, QKV on 96x64
     else if (M >= 2048 && N <= 768 && K >= 512 && gemm_rule() != 1 && gemm_rule() != 2)

@@ -295,6 +295,9 @@ class _Tower:
         # MAPFED_FUSED_QKV_ATTN=0 selects the unfused pair (A/B), "vision" / "text" fuses that tower only
         sel = os.environ.get("MAPFED_FUSED_QKV_ATTN", FUSED_QKV_ATTN_DEFAULT)
         self.fused_qkv_attn = sel == "1" or ("vision" if name == "image_encoder" else "text") in sel.split(",")
+        # GEMM tile rule of this tower's projections: 0 = latency picks (the tower that sets the step), -1 =
+        # work-per-CU-second picks (the tower beside it; MapleEngine.__init__ decides, csrc/gemm.hip text_tile)
+        self.tile = 0
         # this tower's LayerNorm dgamma/dbeta partials, reduced in one launch at the end of its backward
         self.lnb = ops.LNGradBatch(dev)
         self.cs_ws = e(ops.colsum_ws_floats(R, 4 * D), dt=F32)
@@ -339,18 +342,18 @@ class _Tower:
                                       self.QKV[i], self.O[i], self.LSE[i], N, L, H, self.causal)
             else:
                 ops.gemm_nt(h1, self.p(i, "attn.in_proj_weight"), self.QKV[i], bias=self.p(i, "attn.in_proj_bias"),
-                            epilogue=ops.EPI_BIAS)
+                            epilogue=ops.EPI_BIAS, tile=self.tile)
                 ops.attention_fwd(self.QKV[i], N, L, H, self.causal, out=self.O[i], lse=self.LSE[i])
             ops.gemm_nt(self.O[i], self.p(i, "attn.out_proj.weight"), self.X1[i], bias=self.p(i, "attn.out_proj.bias"),
-                        aux_in=x, epilogue=ops.EPI_BIAS_RESID)
+                        aux_in=x, epilogue=ops.EPI_BIAS_RESID, tile=self.tile)
             h2 = self.H2[:R]
             ops.layernorm_fwd(self.X1[i], self.p(i, "ln_2.weight"), self.p(i, "ln_2.bias"), h2, self.mean2[i],
                               self.rstd2[i])
             g = self.G[:R]
             ops.gemm_nt(h2, self.p(i, "mlp.c_fc.weight"), g, bias=self.p(i, "mlp.c_fc.bias"), aux_out=self.Fp[i],
-                        epilogue=ops.EPI_BIAS_GELU)
+                        epilogue=ops.EPI_BIAS_GELU, tile=self.tile)
             ops.gemm_nt(g, self.p(i, "mlp.c_proj.weight"), self.Y[i], bias=self.p(i, "mlp.c_proj.bias"),
-                        aux_in=self.X1[i], epilogue=ops.EPI_BIAS_RESID)
+                        aux_in=self.X1[i], epilogue=ops.EPI_BIAS_RESID, tile=self.tile)
             if i + 1 < self.layers and self.grow[i + 1]:
                 ops.seq_grow(self.Y[i], self.X[i + 1], cap, deep_prompts[i], N, L, self.ncap, N_CTX, D)
         # self.H1 / H2 / G now hold the last layer's (block 11) tensors, kept for its dW
@@ -375,21 +378,22 @@ class _Tower:
             dF, dH, dO, dQKV = self.dF[:R], self.dH[:R], self.dO[:R], self.dQKV[:R]
             trainable_w = i == last
             # ---- MLP: X[i+1] = X1 + c_proj(gelu(c_fc(ln_2(X1))))
-            ops.gemm_nt(dX, self.wt(i, "mlp.c_proj.weight"), dF, aux_in=self.Fp[i], epilogue=ops.EPI_DGELU)
+            ops.gemm_nt(dX, self.wt(i, "mlp.c_proj.weight"), dF, aux_in=self.Fp[i], epilogue=ops.EPI_DGELU,
+                        tile=self.tile)
             if trainable_w:
                 self._dw(dX, self.G[:R], self.g(i, "mlp.c_proj.weight"), self.g(i, "mlp.c_proj.bias"))
-            ops.gemm_nt(dF, self.wt(i, "mlp.c_fc.weight"), dH, epilogue=ops.EPI_NONE)
+            ops.gemm_nt(dF, self.wt(i, "mlp.c_fc.weight"), dH, epilogue=ops.EPI_NONE, tile=self.tile)
             if trainable_w:
                 self._dw(dF, self.H2[:R], self.g(i, "mlp.c_fc.weight"), self.g(i, "mlp.c_fc.bias"))
             self.lnb.bwd(dH, self.X1[i], self.p(i, "ln_2.weight"), self.mean2[i], self.rstd2[i], dX,
                          self.g(i, "ln_2.weight"), self.g(i, "ln_2.bias"), dres=dX)
             # ---- attention: X1 = X + out_proj(attn(ln_1(X)))
-            ops.gemm_nt(dX, self.wt(i, "attn.out_proj.weight"), dO, epilogue=ops.EPI_NONE)
+            ops.gemm_nt(dX, self.wt(i, "attn.out_proj.weight"), dO, epilogue=ops.EPI_NONE, tile=self.tile)
             if trainable_w:
                 self._dw(dX, self.O[i], self.g(i, "attn.out_proj.weight"), self.g(i, "attn.out_proj.bias"))
             ops.attention_bwd(self.QKV[i], self.O[i], dO, self.LSE[i], N, L, H, self.causal, dqkv=dQKV,
                               ws=self.attn_ws)
-            ops.gemm_nt(dQKV, self.wt(i, "attn.in_proj_weight"), dH, epilogue=ops.EPI_NONE)
+            ops.gemm_nt(dQKV, self.wt(i, "attn.in_proj_weight"), dH, epilogue=ops.EPI_NONE, tile=self.tile)
             if trainable_w:
                 self._dw(dQKV, self.H1[:R], self.g(i, "attn.in_proj_weight"), self.g(i, "attn.in_proj_bias"))
             if 1 <= i <= n_prompted and not self.grow[i]:
@@ -466,6 +470,12 @@ class MapleEngine:
         self.txt = _Tower(self, "text_encoder", self.K, self.text_len, d.text_width, d.text_heads, d.text_layers,
                           True, 1)
         self._build_io()
+        # the tower with less projection work per step runs beside the other one (the text tower at c4, the
+        # vision tower at C5): its GEMMs take the work-per-CU-second tiles (csrc/gemm.hip, tile -1)
+        if os.environ.get("MAPFED_SIDE_TILES", "1") != "0":
+            vis_work = self.vis.N * self.vis.L * self.vis.D ** 2
+            txt_work = self.txt.N * self.txt.L * self.txt.D ** 2
+            (self.txt if txt_work <= vis_work else self.vis).tile = -1
         self.side = torch.cuda.Stream(device=self.device)
         self.overlap_towers = True  # False: both towers on the current stream (isolated kernel timing)
         # enqueue (and capture) order of the two towers after the fork: the vision tower (the step's critical
