@@ -66,6 +66,30 @@ def test_gemm8_persistent_matches_staggered(dev, M, N, K):
             assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("M,N,K,epi", [(2926, 512, 2048, 2), (2926, 1536, 512, 1), (6368, 768, 3072, 0),
+                                       (6368, 3072, 768, 3), (6368, 768, 768, 4), (770, 512, 512, 0)])
+def test_gemm_side_tower_tile_hint_is_bit_identical(dev, M, N, K, epi):
+    """tile -1 (the projections of the tower off the critical path: work-per-CU-second tiles, no hipBLASLt route)
+    against the latency picks (tile 0): every tile accumulates each output in the same k order, so the outputs
+    are bit-identical; below 2 048 rows the hint falls back to the latency picks."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + epi)
+    A = torch.randn(M, K, generator=g).half().to(dev)
+    B = (torch.randn(N, K, generator=g) * K ** -0.5).half().to(dev)
+    b = (torch.randn(N, generator=g) * 0.1).half().to(dev)
+    R = torch.randn(M, N, generator=g).half().to(dev)
+    kw = {"bias": b} if epi in (ops.EPI_BIAS, ops.EPI_BIAS_RESID, ops.EPI_BIAS_GELU) else {}
+    if epi in (ops.EPI_BIAS_RESID, ops.EPI_DGELU):
+        kw["aux_in"] = R
+    outs = []
+    for tile in (0, -1):
+        aux_out = torch.empty(M, N, device=dev, dtype=torch.float16) if epi == ops.EPI_BIAS_GELU else None
+        outs.append((ops.gemm_nt(A, B, aux_out=aux_out, epilogue=epi, tile=tile, **kw), aux_out))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    if epi == ops.EPI_BIAS_GELU:
+        assert torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("M,N,K,tile", [(796, 2304, 768, 0), (6368, 768, 3072, 0), (770, 512, 2048, 1),
                                         (130, 44, 64, 3), (257, 1536, 512, 2), (6368, 3072, 768, 0),
                                         # 8-wave phase-pipelined family (tiles 20 = staggered 256x256, 21,
