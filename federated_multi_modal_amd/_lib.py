@@ -44,6 +44,8 @@ SIGNATURES = {
     "mf_small_linear_bwd_batch": [P, I, I, I, I, P],
     "mf_clip_head_fwd": [P, P, I, I, I, P, P, P, P, P, P, P],
     "mf_clip_loss_fwd_bwd": [P, P, P, P, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P],
+    "mf_gemm_resid_ln_supported": [I, I],
+    "mf_gemm_resid_ln": [P, L, P, L, P, P, L, P, L, P, P, P, L, P, P, I, I, I, P],
     "mf_layernorm_bwd_inject": [P, L, P, L, P, P, P, P, L, P, L, P, I, I, P, I, I, I, P],
     "mf_layernorm_fwd_inject": [P, L, P, P, P, L, P, P, I, I, P, I, I, I, P],
     "mf_gemm_splitk": [P, L, I, P, L, I, P, L, I, I, I, P, L, I, I, P],
@@ -71,7 +73,7 @@ SIGNATURES = {
 _VALUE_FUNCS = {"mf_abi_version", "mf_layernorm_bwd_blocks", "mf_colsum_blocks", "mf_optim_chunk_bytes",
                 "mf_optim_chunk_elems", "mf_col_reduce_desc_bytes", "mf_small_linear_desc_bytes",
                 "mf_gemm_splitk_ws_floats", "mf_augment_ws_bytes", "mf_qkv_attention_supported",
-                "mf_gemm_lib_wants"}
+                "mf_gemm_lib_wants", "mf_gemm_resid_ln_supported"}
 # value functions whose return type is not int
 _RESTYPES = {"mf_augment_ws_bytes": ctypes.c_int64}
 

@@ -295,6 +295,9 @@ class _Tower:
         # MAPFED_FUSED_QKV_ATTN=0 selects the unfused pair (A/B), "vision" / "text" fuses that tower only
         sel = os.environ.get("MAPFED_FUSED_QKV_ATTN", FUSED_QKV_ATTN_DEFAULT)
         self.fused_qkv_attn = sel == "1" or ("vision" if name == "image_encoder" else "text") in sel.split(",")
+        # the out-projection, residual add and ln_2 in one launch (full-row tiles, csrc/rowln.hip; D = 768):
+        # bit-identical but 2.8 % slower on the c4 step, so opt-in: MAPFED_FUSED_LN2=1
+        self.fused_ln2 = os.environ.get("MAPFED_FUSED_LN2", "0") == "1" and ops.gemm_resid_ln_supported(D, D)
         # GEMM tile rule of this tower's projections: 0 = latency picks (the tower that sets the step), -1 =
         # work-per-CU-second picks (the tower beside it; MapleEngine.__init__ decides, csrc/gemm.hip text_tile)
         self.tile = 0
@@ -344,11 +347,16 @@ class _Tower:
                 ops.gemm_nt(h1, self.p(i, "attn.in_proj_weight"), self.QKV[i], bias=self.p(i, "attn.in_proj_bias"),
                             epilogue=ops.EPI_BIAS, tile=self.tile)
                 ops.attention_fwd(self.QKV[i], N, L, H, self.causal, out=self.O[i], lse=self.LSE[i])
-            ops.gemm_nt(self.O[i], self.p(i, "attn.out_proj.weight"), self.X1[i], bias=self.p(i, "attn.out_proj.bias"),
-                        aux_in=x, epilogue=ops.EPI_BIAS_RESID, tile=self.tile)
             h2 = self.H2[:R]
-            ops.layernorm_fwd(self.X1[i], self.p(i, "ln_2.weight"), self.p(i, "ln_2.bias"), h2, self.mean2[i],
-                              self.rstd2[i])
+            if self.fused_ln2:  # out_proj + residual + ln_2 in one launch (rowln.hip, bit-identical)
+                ops.gemm_resid_ln(self.O[i], self.p(i, "attn.out_proj.weight"), self.p(i, "attn.out_proj.bias"), x,
+                                  self.X1[i], self.p(i, "ln_2.weight"), self.p(i, "ln_2.bias"), h2, self.mean2[i],
+                                  self.rstd2[i])
+            else:
+                ops.gemm_nt(self.O[i], self.p(i, "attn.out_proj.weight"), self.X1[i],
+                            bias=self.p(i, "attn.out_proj.bias"), aux_in=x, epilogue=ops.EPI_BIAS_RESID, tile=self.tile)
+                ops.layernorm_fwd(self.X1[i], self.p(i, "ln_2.weight"), self.p(i, "ln_2.bias"), h2, self.mean2[i],
+                                  self.rstd2[i])
             g = self.G[:R]
             ops.gemm_nt(h2, self.p(i, "mlp.c_fc.weight"), g, bias=self.p(i, "mlp.c_fc.bias"), aux_out=self.Fp[i],
                         epilogue=ops.EPI_BIAS_GELU, tile=self.tile)

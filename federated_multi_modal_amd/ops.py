@@ -220,6 +220,25 @@ def layernorm_fwd(x, gamma, beta, y=None, mean=None, rstd=None, row_index=None):
 
 
 
+def gemm_resid_ln_supported(N: int, K: int) -> bool:
+    return bool(call("mf_gemm_resid_ln_supported", N, K))
+
+
+def gemm_resid_ln(A, W, bias, R, C, gamma, beta, Y, mean, rstd):
+    """C = fp16(R + fp16(A . W^T + bias)) and Y, mean, rstd = LayerNorm(C) in one launch (rowln.hip;
+    bit-identical to gemm_nt(EPI_BIAS_RESID) + layernorm_fwd).  Probed as a GEMM (its FLOPs; bytes: the
+    product's operands and residual, X1 written, and the LayerNorm's Y / statistics written)."""
+    M, K = A.shape
+    N = W.shape[0]
+    ev = None
+    if _PROBE is not None and _PROBE.wants("gemm"):
+        ev = _PROBE.around(2.0 * M * N * K, _gemm_bytes(M, N, K, C, R) + 2.0 * M * N + 8.0 * M, _gkey())
+    call("mf_gemm_resid_ln", _p(A), _ld(A), _p(W), _ld(W), _p(bias), _p(R), _ld(R), _p(C), _ld(C), _p(gamma),
+         _p(beta), _p(Y), _ld(Y), _p(mean), _p(rstd), M, N, K, _s())
+    _rec(ev)
+    return C, Y
+
+
 def layernorm_fwd_inject(x, gamma, beta, y, mean, rstd, prompt, L, row0, nrows):
     """prompt_inject_fwd(x, prompt, ...) + layernorm_fwd(x, ...) in one kernel (bit-identical)."""
     rows, D = x.shape

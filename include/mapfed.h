@@ -40,6 +40,15 @@ int mf_abi_version(void);
 int mf_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
                const void* bias, const void* aux_in, void* aux_out, int64_t ld_aux, int epilogue, int tile,
                void* stream);
+/* The block's out-projection, residual add and ln_2 in one launch (full-row tiles, rowln.hip):
+ * C = X1 = fp16(R + fp16(A . W^T + bias)), Y = LayerNorm(X1; gamma, beta, eps 1e-5) fp16, mean / rstd fp32
+ * per row.  Bit-identical to mf_gemm_nt(EPI_BIAS_RESID) + mf_layernorm_fwd.  N = 768, K % 32 == 0
+ * (mf_gemm_resid_ln_supported).  Replaces clip/model.py:303-305 (out_proj), 350 (x + attn) and 351's
+ * ln_2 (153-159).                                                                                 */
+int mf_gemm_resid_ln_supported(int N, int K);
+int mf_gemm_resid_ln(const void* A, int64_t lda, const void* W, int64_t ldw, const void* bias, const void* R,
+                     int64_t ldr, void* C, int64_t ldc, const float* gamma, const float* beta, void* Y, int64_t ldy,
+                     float* mean, float* rstd, int M, int N, int K, void* stream);
 /* General layouts: C[M,N] = epilogue(op(A) . op(B)^T) with
  *   a_kmajor = 0: A[m][k] at A[m*lda + k]  |  1: A[k*lda + m]   (e.g. dY^T of a weight gradient)
  *   b_kmajor = 0: B[n][k] at B[n*ldb + k]  |  1: B[k*ldb + n]   (e.g. nn.Linear W [out][in] in dX = dY . W)

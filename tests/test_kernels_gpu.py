@@ -66,6 +66,30 @@ def test_gemm8_persistent_matches_staggered(dev, M, N, K):
             assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("M,K", [(6368, 768), (1000, 768), (63, 256), (3184, 768)])
+def test_gemm_resid_ln_matches_the_pair(dev, M, K):
+    """mf_gemm_resid_ln (out-projection + residual + ln_2 on full-row tiles, one launch) against
+    mf_gemm_nt(EPI_BIAS_RESID) + mf_layernorm_fwd: X1, h2, mean and rstd bit-identical (ragged M included)."""
+    N = 768
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    A = torch.randn(M, K, generator=g).half().to(dev)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).half().to(dev)
+    b = (torch.randn(N, generator=g) * 0.1).half().to(dev)
+    R = torch.randn(M, N, generator=g).half().to(dev)
+    gamma = (1 + 0.1 * torch.randn(N, generator=g)).to(dev)
+    beta = (0.1 * torch.randn(N, generator=g)).to(dev)
+    X1a = ops.gemm_nt(A, W, bias=b, aux_in=R, epilogue=ops.EPI_BIAS_RESID)
+    Ya, ma, ra = ops.layernorm_fwd(X1a, gamma, beta)
+    X1b = torch.empty_like(X1a)
+    Yb = torch.empty_like(Ya)
+    mb, rb = torch.empty_like(ma), torch.empty_like(ra)
+    ops.gemm_resid_ln(A, W, b, R, X1b, gamma, beta, Yb, mb, rb)
+    torch.cuda.synchronize()
+    assert torch.equal(X1a, X1b)
+    assert torch.equal(Ya, Yb)
+    assert torch.equal(ma, mb) and torch.equal(ra, rb)
+
+
 @pytest.mark.parametrize("M,N,K,epi", [(2926, 512, 2048, 2), (2926, 1536, 512, 1), (6368, 768, 3072, 0),
                                        (6368, 3072, 768, 3), (6368, 768, 768, 4), (770, 512, 512, 0)])
 def test_gemm_side_tower_tile_hint_is_bit_identical(dev, M, N, K, epi):
