@@ -80,7 +80,9 @@ __global__ void sumsq_chunks_kernel(const f16* __restrict__ g16, const float* __
 // out[0] = total norm, out[1] = clip coef, out[2] = 1 if total is finite else 0
 __global__ __launch_bounds__(1024) void clip_coef_kernel(const float* __restrict__ part,
                                                          const Chunk* __restrict__ chunks, int nchunks,
-                                                         float max_norm, float* __restrict__ out) {
+                                                         float max_norm, float* __restrict__ out,
+                                                         float* __restrict__ hyper = nullptr,
+                                                         const float* __restrict__ halt_src = nullptr) {
   __shared__ float sv[1024];
   __shared__ int sseg[1024];
   __shared__ float red[16];
@@ -135,6 +137,8 @@ __global__ __launch_bounds__(1024) void clip_coef_kernel(const float* __restrict
     out[0] = total;
     out[1] = coef;
     out[2] = isfinite(total) ? 1.f : 0.f;
+    // the step's halt latch (torch.maximum(hyper[4], loss non-finite flag)) for the SGD launch that follows
+    if (hyper) hyper[4] = fmaxf(hyper[4], halt_src[0]);
   }
 }
 
@@ -166,10 +170,9 @@ __global__ void sgd_kernel(T* __restrict__ p, T* __restrict__ g, T* __restrict__
 // sgd_kernel on 8 consecutive elements per thread (16-byte fp16 / 2 x 16-byte fp32 accesses), the same
 // per-element arithmetic; n % 8 == 0 and 16-byte aligned buffers
 template <typename T>
-__global__ void sgd8_kernel(T* __restrict__ p, T* __restrict__ g, T* __restrict__ buf, int64_t n8,
-                            const float* __restrict__ coef_ptr, const float* __restrict__ hyper) {
+MF_DEV void sgd8_body(T* __restrict__ p, T* __restrict__ g, T* __restrict__ buf, int64_t n8, int64_t i,
+                      const float* __restrict__ coef_ptr, const float* __restrict__ hyper) {
   using V = typename std::conditional<std::is_same<T, f16>::value, f16x8, float __attribute__((ext_vector_type(8)))>::type;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n8 || hyper[4] != 0.f) return;
   const float coef = coef_ptr[1];
   const float lr = hyper[0], momentum = hyper[1], wd = hyper[2];
@@ -192,6 +195,23 @@ __global__ void sgd8_kernel(T* __restrict__ p, T* __restrict__ g, T* __restrict_
   ((V*)g)[i] = gv;
   ((V*)buf)[i] = bv;
   ((V*)p)[i] = pv;
+}
+
+template <typename T>
+__global__ void sgd8_kernel(T* __restrict__ p, T* __restrict__ g, T* __restrict__ buf, int64_t n8,
+                            const float* __restrict__ coef_ptr, const float* __restrict__ hyper) {
+  sgd8_body<T>(p, g, buf, n8, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, coef_ptr, hyper);
+}
+
+// both flat buffers' SGD in one launch: blocks [0, nb16) update the fp16 trainables, the rest the fp32 ones
+__global__ void sgd8_both_kernel(f16* __restrict__ p16, f16* __restrict__ g16, f16* __restrict__ b16, int64_t n16_8,
+                                 float* __restrict__ p32, float* __restrict__ g32, float* __restrict__ b32,
+                                 int64_t n32_8, unsigned nb16, const float* __restrict__ coef_ptr,
+                                 const float* __restrict__ hyper) {
+  if (blockIdx.x < nb16)
+    sgd8_body<f16>(p16, g16, b16, n16_8, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, coef_ptr, hyper);
+  else
+    sgd8_body<float>(p32, g32, b32, n32_8, (int64_t)(blockIdx.x - nb16) * blockDim.x + threadIdx.x, coef_ptr, hyper);
 }
 
 // bucket[0:n16] = float(p16), bucket[n16:n16+n32] = p32
@@ -289,6 +309,34 @@ extern "C" int mf_clip_grad_norm(const void* g16, const float* g32, const void* 
   clip_coef_kernel<<<1, 1024, 0, st>>>(part, (const Chunk*)chunks, nchunks, max_norm, out);
   MF_CHECK_LAUNCH();
   return 0;
+}
+
+// The whole optimizer step in three launches: clip_grad_norm_ (partial sums, then the coefficient, which also
+// latches hyper[4] = max(hyper[4], *halt_src) -- the torch.maximum the engine used to launch), then SGD over the
+// fp16 and the fp32 flat buffers in one launch.  Bit-identical to mf_clip_grad_norm + two mf_sgd_step.
+extern "C" int mf_sgd_step(void* p, void* g, void* buf, int64_t n, int is16, const float* coef, const float* hyper,
+                           void* stream);
+extern "C" int mf_optimizer_step(void* p16, void* g16, void* b16, int64_t n16, float* p32, float* g32, float* b32,
+                                 int64_t n32, const void* chunks, int nchunks, float max_norm, float* part, float* out,
+                                 float* hyper, const float* halt_src, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (nchunks > 0) {
+    sumsq_chunks_kernel<<<nchunks, 256, 0, st>>>((const f16*)g16, g32, (const Chunk*)chunks, part);
+    MF_CHECK_LAUNCH();
+  }
+  clip_coef_kernel<<<1, 1024, 0, st>>>(part, (const Chunk*)chunks, nchunks, max_norm, out, hyper, halt_src);
+  MF_CHECK_LAUNCH();
+  const bool vec16 = n16 % 8 == 0 && (uintptr_t)p16 % 32 == 0 && (uintptr_t)g16 % 32 == 0 && (uintptr_t)b16 % 32 == 0;
+  const bool vec32 = n32 % 8 == 0 && (uintptr_t)p32 % 32 == 0 && (uintptr_t)g32 % 32 == 0 && (uintptr_t)b32 % 32 == 0;
+  if (vec16 && vec32 && n16 + n32 > 0) {
+    const unsigned nb16 = nblk(n16 / 8), nb32 = nblk(n32 / 8);
+    sgd8_both_kernel<<<nb16 + nb32, 256, 0, st>>>((f16*)p16, (f16*)g16, (f16*)b16, n16 / 8, p32, g32, b32, n32 / 8,
+                                                  nb16, out, hyper);
+    MF_CHECK_LAUNCH();
+    return 0;
+  }
+  int rc = mf_sgd_step(p16, g16, b16, n16, 1, out, hyper, stream);
+  return rc ? rc : mf_sgd_step(p32, g32, b32, n32, 0, out, hyper, stream);
 }
 
 extern "C" int mf_sgd_step(void* p, void* g, void* buf, int64_t n, int is16, const float* coef,

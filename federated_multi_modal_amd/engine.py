@@ -490,6 +490,8 @@ class MapleEngine:
         # path) first, so its launches are dispatched ahead of the text tower's (MAPFED_TOWER_ORDER=text: the
         # text tower first, the A/B baseline)
         self.vision_first = os.environ.get("MAPFED_TOWER_ORDER", "vision") != "text"
+        # the optimizer step as mf_optimizer_step (MAPFED_FUSED_OPTIM=0: the four-call form, A/B knob)
+        self.fused_optim = os.environ.get("MAPFED_FUSED_OPTIM", "1") != "0"
         self.step_count = 0
         self.momentum_initialised = False
 
@@ -919,11 +921,16 @@ class MapleEngine:
         loss") at that step before its backward (trainers/maple.py:375-376), so neither that step nor any
         later one of the epoch updates the weights; the SGD kernels skip while halt is set.  The trainer
         clears it at the start of an epoch and reports the failure (MaPLe.run_epoch)."""
-        torch.maximum(self.hyper[4:5], self.loss_out[3:4], out=self.hyper[4:5])
-        ops.clip_grad_norm(self.gflat16, self.gflat32, self.chunks, self.nchunks, self.cfg.max_grad_norm,
-                           self.norm_part, self.clip_out)
-        ops.sgd_step(self.flat16, self.gflat16, self.mom16, self.clip_out, self.hyper)
-        ops.sgd_step(self.flat32, self.gflat32, self.mom32, self.clip_out, self.hyper)
+        if self.fused_optim:  # the same four steps in three launches (mf_optimizer_step, bit-identical)
+            ops.optimizer_step(self.flat16, self.gflat16, self.mom16, self.flat32, self.gflat32, self.mom32, self.chunks,
+                               self.nchunks, self.cfg.max_grad_norm, self.norm_part, self.clip_out, self.hyper,
+                               self.loss_out[3:4])
+        else:
+            torch.maximum(self.hyper[4:5], self.loss_out[3:4], out=self.hyper[4:5])
+            ops.clip_grad_norm(self.gflat16, self.gflat32, self.chunks, self.nchunks, self.cfg.max_grad_norm,
+                               self.norm_part, self.clip_out)
+            ops.sgd_step(self.flat16, self.gflat16, self.mom16, self.clip_out, self.hyper)
+            ops.sgd_step(self.flat32, self.gflat32, self.mom32, self.clip_out, self.hyper)
         # the momentum buffers now exist (first_step -> 0) unless the update was skipped
         self.hyper[3:4].mul_(self.hyper[4:5])  # device ops, legal inside graph capture
 
