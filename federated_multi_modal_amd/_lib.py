@@ -59,7 +59,7 @@ SIGNATURES = {
     "mf_optim_chunk_elems": [],
     "mf_clip_grad_norm": [P, P, P, I, F, P, P, P],
     "mf_sgd_step": [P, P, P, L, I, P, P, P],
-    "mf_optimizer_step": [P, P, P, L, P, P, P, L, P, I, F, P, P, P, P, P],
+    "mf_optimizer_step": [P, P, P, L, P, P, P, L, P, I, F, P, P, P, P, P, P],
     "mf_fedavg_pack": [P, L, P, L, P, P, P],
     "mf_fedavg_unpack": [P, P, L, P, L, P, P, P],
     "mf_fedavg_reduce_ordered": [P, I, L, L, P, P],

@@ -82,7 +82,8 @@ __global__ __launch_bounds__(1024) void clip_coef_kernel(const float* __restrict
                                                          const Chunk* __restrict__ chunks, int nchunks,
                                                          float max_norm, float* __restrict__ out,
                                                          float* __restrict__ hyper = nullptr,
-                                                         const float* __restrict__ halt_src = nullptr) {
+                                                         const float* __restrict__ halt_src = nullptr,
+                                                         const int* __restrict__ halt_src2 = nullptr) {
   __shared__ float sv[1024];
   __shared__ int sseg[1024];
   __shared__ float red[16];
@@ -138,7 +139,10 @@ __global__ __launch_bounds__(1024) void clip_coef_kernel(const float* __restrict
     out[1] = coef;
     out[2] = isfinite(total) ? 1.f : 0.f;
     // the step's halt latch (torch.maximum(hyper[4], loss non-finite flag)) for the SGD launch that follows
-    if (hyper) hyper[4] = fmaxf(hyper[4], halt_src[0]);
+    if (hyper) {
+      const float h = fmaxf(hyper[4], halt_src[0]);
+      hyper[4] = halt_src2 ? fmaxf(h, (float)halt_src2[0]) : h;
+    }
   }
 }
 
@@ -312,19 +316,21 @@ extern "C" int mf_clip_grad_norm(const void* g16, const float* g32, const void* 
 }
 
 // The whole optimizer step in three launches: clip_grad_norm_ (partial sums, then the coefficient, which also
-// latches hyper[4] = max(hyper[4], *halt_src) -- the torch.maximum the engine used to launch), then SGD over the
-// fp16 and the fp32 flat buffers in one launch.  Bit-identical to mf_clip_grad_norm + two mf_sgd_step.
+// latches hyper[4] = max(hyper[4], *halt_src, *input_flag) -- the two torch.maximum launches the engine used to
+// make, at the step's start for the input check and here for the loss), then SGD over the fp16 and the fp32 flat
+// buffers in one launch.  Bit-identical to mf_clip_grad_norm + two mf_sgd_step.  input_flag may be null.
 extern "C" int mf_sgd_step(void* p, void* g, void* buf, int64_t n, int is16, const float* coef, const float* hyper,
                            void* stream);
 extern "C" int mf_optimizer_step(void* p16, void* g16, void* b16, int64_t n16, float* p32, float* g32, float* b32,
                                  int64_t n32, const void* chunks, int nchunks, float max_norm, float* part, float* out,
-                                 float* hyper, const float* halt_src, void* stream) {
+                                 float* hyper, const float* halt_src, const int* input_flag, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (nchunks > 0) {
     sumsq_chunks_kernel<<<nchunks, 256, 0, st>>>((const f16*)g16, g32, (const Chunk*)chunks, part);
     MF_CHECK_LAUNCH();
   }
-  clip_coef_kernel<<<1, 1024, 0, st>>>(part, (const Chunk*)chunks, nchunks, max_norm, out, hyper, halt_src);
+  clip_coef_kernel<<<1, 1024, 0, st>>>(part, (const Chunk*)chunks, nchunks, max_norm, out, hyper, halt_src,
+                                       input_flag);
   MF_CHECK_LAUNCH();
   const bool vec16 = n16 % 8 == 0 && (uintptr_t)p16 % 32 == 0 && (uintptr_t)g16 % 32 == 0 && (uintptr_t)b16 % 32 == 0;
   const bool vec32 = n32 % 8 == 0 && (uintptr_t)p32 % 32 == 0 && (uintptr_t)g32 % 32 == 0 && (uintptr_t)b32 % 32 == 0;

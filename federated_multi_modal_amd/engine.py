@@ -871,7 +871,8 @@ class MapleEngine:
         ops.nonfinite_flag(self.img_in, self.input_flag)
         if self.soft_labels:
             ops.nonfinite_flag(self.soft_label_in, self.input_flag)
-        torch.maximum(self.hyper[4:5], self.input_flag.to(F32), out=self.hyper[4:5])
+        if not self.fused_optim:  # (else mf_optimizer_step latches the input flag into hyper[4] at the step's end)
+            torch.maximum(self.hyper[4:5], self.input_flag.to(F32), out=self.hyper[4:5])
         main = torch.cuda.current_stream(self.device)
         side = self.side if self.overlap_towers else main
         side.wait_stream(main)
@@ -924,7 +925,7 @@ class MapleEngine:
         if self.fused_optim:  # the same four steps in three launches (mf_optimizer_step, bit-identical)
             ops.optimizer_step(self.flat16, self.gflat16, self.mom16, self.flat32, self.gflat32, self.mom32, self.chunks,
                                self.nchunks, self.cfg.max_grad_norm, self.norm_part, self.clip_out, self.hyper,
-                               self.loss_out[3:4])
+                               self.loss_out[3:4], self.input_flag)
         else:
             torch.maximum(self.hyper[4:5], self.loss_out[3:4], out=self.hyper[4:5])
             ops.clip_grad_norm(self.gflat16, self.gflat32, self.chunks, self.nchunks, self.cfg.max_grad_norm,

@@ -572,13 +572,14 @@ def sgd_step(p, g, buf, coef, hyper):
     _rec(ev)
 
 
-def optimizer_step(p16, g16, b16, p32, g32, b32, chunks, nchunks, max_norm, part, out, hyper, halt_src):
-    """clip_grad_norm + sgd_step(fp16) + sgd_step(fp32), with hyper[4] = max(hyper[4], halt_src[0]) folded in:
-    three launches, bit-identical (mf_optimizer_step)."""
+def optimizer_step(p16, g16, b16, p32, g32, b32, chunks, nchunks, max_norm, part, out, hyper, halt_src,
+                   input_flag=None):
+    """clip_grad_norm + sgd_step(fp16) + sgd_step(fp32), with hyper[4] = max(hyper[4], halt_src[0], input_flag[0])
+    folded in: three launches, bit-identical (mf_optimizer_step)."""
     nb = g16.numel() * 2.0 + g32.numel() * 4.0 + p16.numel() * 10.0 + p32.numel() * 20.0
     ev = _hbm("optimizer_step", nb)  # every gradient read twice; p, g, momentum read and written
     call("mf_optimizer_step", _p(p16), _p(g16), _p(b16), p16.numel(), _p(p32), _p(g32), _p(b32), p32.numel(), _p(chunks),
-         nchunks, float(max_norm), _p(part), _p(out), _p(hyper), _p(halt_src), _s())
+         nchunks, float(max_norm), _p(part), _p(out), _p(hyper), _p(halt_src), _p(input_flag), _s())
     _rec(ev)
 
 

@@ -211,11 +211,12 @@ int mf_clip_grad_norm(const void* g16, const float* g32, const void* chunks, int
 int mf_sgd_step(void* p, void* g, void* buf, int64_t n, int is16, const float* coef, const float* hyper,
                 void* stream);
 /* The optimizer step in three launches (clip partial sums, coefficient + halt latch, SGD over both flat
- * buffers): mf_clip_grad_norm + mf_sgd_step(fp16) + mf_sgd_step(fp32), with hyper[4] = max(hyper[4], *halt_src)
- * (the step's non-finite-loss flag) folded into the coefficient launch.  Bit-identical to those calls.        */
+ * buffers): mf_clip_grad_norm + mf_sgd_step(fp16) + mf_sgd_step(fp32), with hyper[4] = max(hyper[4], *halt_src,
+ * *input_flag) (the step's non-finite-loss flag and its non-finite-input flag, input_flag nullable) folded into
+ * the coefficient launch.  Bit-identical to those calls.                                                     */
 int mf_optimizer_step(void* p16, void* g16, void* b16, int64_t n16, float* p32, float* g32, float* b32, int64_t n32,
                       const void* chunks, int nchunks, float max_norm, float* part, float* out, float* hyper,
-                      const float* halt_src, void* stream);
+                      const float* halt_src, const int* input_flag, void* stream);
 /* bucket[0:n16+n32] = this client's trainables as fp32 (0 if *invalid_flag), bucket[n16+n32] = its vote
  * (1 valid / 0 invalid); after an all-reduce(SUM) of the n16+n32+1 floats, unpack writes
  * fp16(sum / n_valid) into every trainable and into the global copy g16/g32, n_valid read from

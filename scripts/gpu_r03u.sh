@@ -5,7 +5,7 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py tests/test_trainers_gpu.py tests/test_kernels_gpu.py -k "sgd or clip or engine or nonfinite or halt or step or failed" \
+timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py tests/test_trainers_gpu.py tests/test_kernels_gpu.py -k "sgd or clip or engine or nonfinite or halt or step or failed or input" \
   -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_u.log 2>&1
 rc=$?; echo "tests rc=$rc"; grep -E "^FAILED|passed|failed" gpurun_out/pytest_u.log | tail -3
 [ $rc -eq 0 ] || exit $rc
