@@ -148,17 +148,75 @@ def side_config(name, dev, world, rank, steps=5, warmup=2, seed=0, eot_truncate=
             fam[tower] = {"launches": p["launches"], "avg_launch_us": p["avg_us"], "tflops": p["tflops"],
                           "mfma_frac": p["tflops"] * 1e12 / MFMA_PEAK_F16, "flop_per_launch": p["flops_per_launch"]}
     step_flop = B * FLOP_PER_IMAGE + K * FLOP_PER_CLASS
+    # FLOP the step executes: the algorithmic count, except with the EOT-truncated text tower, whose rate and
+    # MFMA fraction are priced on what it runs (no fraction counts FLOP that did not execute)
+    exec_flop = B * FLOP_PER_IMAGE + K * text_flop_per_class(e.text_len)
     out = {"workload": f"{name}: {desc}", "value": world * B * steps / el, "unit": "images/s",
            "ms_per_step": 1e3 * el / steps, "steps": steps, "loss": loss,
-           "model_tflops": world * step_flop * steps / el / 1e12,
-           "model_mfma_frac": step_flop * steps / el / MFMA_PEAK_F16, "gemm_by_tower": fam or None}
+           "model_tflops": world * exec_flop * steps / el / 1e12,
+           "model_mfma_frac": exec_flop * steps / el / MFMA_PEAK_F16, "gemm_by_tower": fam or None}
     if eot_truncate:
         Lt = e.text_len
-        out.update(text_tokens=Lt, executed_gflop_per_step=(B * FLOP_PER_IMAGE + K * text_flop_per_class(Lt)) / 1e9,
+        out.update(text_tokens=Lt, executed_gflop_per_step=exec_flop / 1e9,
                    algorithmic_gflop_per_step=step_flop / 1e9,
+                   flop_basis="model_tflops / model_mfma_frac: executed FLOP (text tower on text_tokens rows)",
                    parity="logits and loss bit-identical to the 77-token tower; gradients equal up to fp32 summation "
                           "order (tests/test_engine_gpu.py::test_eot_truncated_text_tower_matches_full)")
     del g, e
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+def fed_round_wall(name, world, rank, epochs=10, test_images=1000, shots=16, seed=1):
+    """The metric's second half, the FedAvg round wall-time (local epochs + tests +
+    exchange), through the reference's trainer API: MaPLeFederated.train() (trainers/maple_fed.py:228-303)
+    with one client per rank, FED.LOCAL_EPOCHS local epochs per round, each epoch a pass over the client's
+    `shots`-shot train split followed by test() over `test_images` images (trainers/maple.py:629-681), then
+    the FedAvg exchange (started before the last test()), the global-state read and client 0's round test.
+    Two rounds run; round 2 is reported (round 1 also captures the step graphs and builds the eval engine).
+    Synthetic splits repeat 64 generated images (the host PRNG stays out of the run; the device work per
+    batch is the same).  Times are host wall seconds, max over ranks; the trainer reads them at the host
+    syncs it makes anyway (MaPLeFederated.round_times)."""
+    import contextlib
+    import io
+    import tempfile
+    from federated_multi_modal_amd.config import extend_cfg, get_cfg_default
+    from federated_multi_modal_amd.trainers import build_trainer
+    J, K, B, desc = CONFIGS[name]
+    cfg = get_cfg_default()
+    extend_cfg(cfg)
+    cfg.merge_from_file(str(ROOT / "configs/trainers/MaPLeFederated/vit_b16_c2_ep5_batch4_2ctx_cross_datasets.yaml"))
+    out_dir = tempfile.mkdtemp(prefix="mapfed_round_")
+    cfg.merge_from_list(["TRAINER.NAME", "MaPLeFederated", "SEED", seed, "OUTPUT_DIR", out_dir, "VERBOSE", False,
+                         "FED.NUM_CLIENTS", world, "FED.NUM_ROUNDS", 2, "FED.LOCAL_EPOCHS", epochs,
+                         "MODEL.NUM_CLASSES", K, "DATASET.NUM_SHOTS", shots, "DATALOADER.TRAIN_X.BATCH_SIZE", B,
+                         "FED.SYNTHETIC_TEST_IMAGES", test_images, "FED.SYNTHETIC_UNIQUE_IMAGES", 64,
+                         "TRAINER.MAPLE.PROMPT_DEPTH", J])
+    cfg.freeze()
+    with contextlib.redirect_stdout(io.StringIO()):  # the trainer's per-epoch prints (stdout carries the JSON line)
+        tr = build_trainer(cfg)
+        tr.train()
+    rec = dict(tr.round_times[-1])
+    keys = [k for k, v in rec.items() if k.endswith("_s")]
+    if world > 1:
+        t = torch.tensor([rec[k] for k in keys], device=tr.device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        rec.update(zip(keys, t.tolist()))
+    c0 = tr.clients[0]
+    n_train = len(c0.dm.train_loader) * B
+    out = {"workload": f"{name}: {desc}; {shots}-shot train split ({n_train} images, {len(c0.dm.train_loader)} "
+                       f"steps per epoch), {test_images}-image test split in batches of "
+                       f"{cfg.DATALOADER.TEST.BATCH_SIZE}, {epochs} local epochs, {world} client(s), one per rank",
+           "round_wall_s": rec["wall_s"],
+           "split_s": {k: rec[k] for k in keys if k != "wall_s"},
+           "steps": rec["steps"], "train_ms_per_step": 1e3 * rec["local_train_s"] / max(rec["steps"], 1),
+           "test_images_per_s": epochs * test_images * len(tr.clients) / max(rec["local_test_s"], 1e-9),
+           "valid_clients": rec["valid"], "round": rec["round"],
+           "note": "max over ranks per phase; local_train_s = the graph-replayed client steps of all local epochs "
+                   "(one host sync per epoch), local_test_s = the per-epoch test() passes (text features encoded once "
+                   "per pass), fedavg_exposed_s = the exchange's wait + unpack after the client loop"}
+    del tr
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return out
@@ -177,6 +235,7 @@ def main():
     ap.add_argument("--no-eot-mode", action="store_true", help="skip the separately reported EOT-truncated run")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (K=1000 text side) side metric")
     ap.add_argument("--no-caption-mode", action="store_true", help="skip the caption-batch (K19) side metric")
+    ap.add_argument("--no-round", action="store_true", help="skip the FedAvg round wall-time (trainer) runs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -288,9 +347,13 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el_t = float(t.item())
         Lt = eng_t.text_len
+        exec_flop_t = B * FLOP_PER_IMAGE + K * text_flop_per_class(Lt)
         eot_mode = {"value": world * B * args.steps / el_t, "unit": "images/s", "ms_per_step": 1e3 * el_t / args.steps,
                     "text_tokens": Lt, "loss": eng_t.loss(),
-                    "executed_gflop_per_step": (B * FLOP_PER_IMAGE + K * text_flop_per_class(Lt)) / 1e9,
+                    "model_tflops": world * exec_flop_t * args.steps / el_t / 1e12,
+                    "model_mfma_frac": exec_flop_t * args.steps / el_t / MFMA_PEAK_F16,
+                    "flop_basis": "model_tflops / model_mfma_frac: executed FLOP (text tower on text_tokens rows)",
+                    "executed_gflop_per_step": exec_flop_t / 1e9,
                     "algorithmic_gflop_per_step": (B * FLOP_PER_IMAGE + K * FLOP_PER_CLASS) / 1e9,
                     "parity": "logits and loss bit-identical to the 77-token tower; gradients equal up to fp32 "
                               "summation order (tests/test_engine_gpu.py::test_eot_truncated_text_tower_matches_full)"}
@@ -477,23 +540,24 @@ def main():
         hbm_roof[key] = {"launches_per_step": a["launches"] // 2, "avg_launch_us": a["avg_us"],
                          "bytes_per_launch": a["bytes_per_launch"], "gbs": a["gbs"], "hbm_frac": a["gbs"] * 1e9 / HBM_PEAK}
 
-    # HBM traffic of the dominant kernel family, per launch, from the rocprofv3 PMC passes of this same
-    # command (scripts/gpu_pmc.sh -> profiles/*_<config>_pmc_summary.json: FETCH_SIZE doubled per
-    # MI355X_MICROARCH.md §HBM + WRITE_SIZE, memory-side counters); None when no summary exists
-    traffic = None
-    traffic_src = None
+    # HBM traffic of the dominant kernel family, per launch, from rocprofv3 PMC passes over exactly the launches
+    # this probe times (tests/diagnostics/gemm_traffic.py: the same two eager steps, FETCH_SIZE x 2 + WRITE_SIZE
+    # per MI355X_MICROARCH.md §HBM, memory-side counters) -> profiles/r<round>_v<n>_<config>_gemm_traffic.json,
+    # which also holds the algorithmic bytes of those same launches; None when no such file exists
+    traffic = traffic_alg = traffic_src = None
+
     def _ver(path):  # r<round>_v<n>_... -> (round, n)
         m = re.match(r"r(\d+)_v(\d+)_", path.name)
         return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
 
-    pmc = sorted((ROOT / "profiles").glob(f"*_{args.config}_pmc_summary.json"), key=_ver)
+    pmc = sorted((ROOT / "profiles").glob(f"*_{args.config}_gemm_traffic.json"), key=_ver)
     if pmc and args.roofline_kernel == "gemm":
         try:
-            fam = json.loads(pmc[-1].read_text()).get("gemm", {})
-            traffic = fam.get("hbm_bytes_per_launch")
+            tj = json.loads(pmc[-1].read_text())
+            traffic, traffic_alg = tj["traffic_bytes_per_launch"], tj["algorithmic_bytes_per_launch"]
             traffic_src = str(pmc[-1].relative_to(ROOT))
-        except (OSError, ValueError):
-            traffic = None
+        except (OSError, ValueError, KeyError):
+            traffic = traffic_alg = None
 
     step_flop = B * FLOP_PER_IMAGE + K * FLOP_PER_CLASS
     value = world * B * args.steps / elapsed
@@ -501,8 +565,12 @@ def main():
         roof = {"bound": "mfma", "achieved": ps["tflops"], "peak": MFMA_PEAK_F16 / 1e12, "unit": "TFLOP/s",
                 "frac": ps["tflops"] * 1e12 / MFMA_PEAK_F16, "traffic": traffic, "traffic_unit": "bytes/launch",
                 "traffic_source": traffic_src, "algorithmic_bytes_per_launch": ps["bytes_per_launch"],
-                "kernel": "GEMM family: gemm_nt_kernel + gemm8(s)_kernel + the hipBLASLt-routed plain / bias-only products "
-                          "(vision in-projection, c_fc dX; csrc/blaslt.hip) -- every projection GEMM, fwd+bwd",
+                "traffic_source_algorithmic_bytes_per_launch": traffic_alg,
+                "traffic_over_algorithmic": traffic / traffic_alg if traffic and traffic_alg else None,
+                "kernel": "GEMM family: the hand-written gemm_nt_kernel / gemm8(s)_kernel launches (csrc/gemm.hip) -- "
+                          "every projection GEMM of both towers, fwd + bwd" + (
+                              "" if not ops.gemm_lib_wants(6368, 2304, 768, ops.EPI_BIAS) else
+                              " + the hipBLASLt-routed products (MAPFED_GEMM_LIB=1)"),
                 "launches_per_step": ps["launches"] // 2,
                 "avg_launch_us": ps["avg_us"], "flop_per_launch": ps["flops_per_launch"]}
         by_tower = {}
@@ -522,6 +590,15 @@ def main():
         roof = {"bound": "mfma", "achieved": ps["tflops"], "peak": MFMA_PEAK_F16 / 1e12, "unit": "TFLOP/s",
                 "frac": ps["tflops"] * 1e12 / MFMA_PEAK_F16, "traffic": None, "kernel": "attention_fwd_kernel",
                 "avg_launch_us": ps["avg_us"], "flop_per_launch": ps["flops_per_launch"]}
+
+    # ---------------- FedAvg round wall-time through MaPLeFederated.train() at the reference's cadence, at the
+    # C3 client shape (configs[2]) and at this workload's (the metric's second half; beside `value`)
+    fed_round = None
+    if not args.no_round:
+        fed_round = {}
+        for cname in dict.fromkeys(("c3", args.config)):
+            log(f"[bench] FedAvg round wall-time ({cname}) ...")
+            fed_round[cname] = fed_round_wall(cname, world, rank)
 
     c5 = None
     if args.config == "c4" and not args.no_c5:
@@ -554,6 +631,7 @@ def main():
         "fedavg_allreduce_ms": fedavg_allreduce_ms,
         "fedavg_bucket_mb": 4.0 * (eng.n16 + eng.n32 + 1) / 1e6,
         "fedavg_valid_clients": fed.n_valid(),
+        "fedavg_round_wall": fed_round,
         "eot_truncated_mode": eot_mode,
         "caption_mode": cap_mode,
         "c5_side": c5,

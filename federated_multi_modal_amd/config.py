@@ -197,7 +197,11 @@ def extend_cfg(cfg: CfgNode) -> None:
     cfg.FED = CfgNode(dict(NUM_CLIENTS=2, NUM_ROUNDS=30, LOCAL_EPOCHS=10,
                            # MI355X additions (federated.py): the bucket exchange -- "ordered" (all_gather +
                            # client-order sum, bit-identical to safe_average_weights) or "allreduce"
-                           AGGREGATION="ordered"))
+                           AGGREGATION="ordered",
+                           # size of each client's synthetic test split (no DATASET.ROOT); 0: one test batch
+                           SYNTHETIC_TEST_IMAGES=0,
+                           # > 0: the synthetic splits repeat that many generated images (bench timing runs)
+                           SYNTHETIC_UNIQUE_IMAGES=0))
 
 
 def reset_cfg(cfg: CfgNode, args) -> None:

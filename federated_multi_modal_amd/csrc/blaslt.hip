@@ -116,7 +116,9 @@ extern "C" int mf_gemm_lib(const void* A, int64_t lda, const void* B, int64_t ld
       good = good && hipblasLtMatrixLayoutCreate(&p->lc, HIP_R_16F, N, M, ldc) == HIPBLAS_STATUS_SUCCESS;
       hipblasLtMatmulPreference_t pref = nullptr;
       good = good && hipblasLtMatmulPreferenceCreate(&pref) == HIPBLAS_STATUS_SUCCESS;
-      const uint64_t wsb = s.ws_bytes;
+      // workspace-free algorithms only: the vision and text towers' products run on two streams at once and a
+      // shared workspace would let two concurrent launches overwrite each other's partial sums
+      const uint64_t wsb = 0;
       good = good && hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb,
                                                            sizeof(wsb)) == HIPBLAS_STATUS_SUCCESS;
       hipblasLtMatmulHeuristicResult_t res[1];
@@ -129,7 +131,7 @@ extern "C" int mf_gemm_lib(const void* A, int64_t lda, const void* B, int64_t ld
         return mf_set_error("mf_gemm_lib: no hipBLASLt algorithm for this product", -1);
       }
       p->algo = res[0].algo;
-      p->ws = res[0].workspaceSize;
+      p->ws = 0;
       p->ok = true;
     }
   }

@@ -822,6 +822,160 @@ __global__ __launch_bounds__(512) void gemm8s_kernel(GemmArgs g) {
   MF_STAMP(3);
 }
 
+// ------------------------------------------------------------------------------------------------
+// gemm4r: BM x BN tile on 4 waves (2 x 2, one wave per SIMD), each wave a (BM/2) x (BN/2) block of 16x16 MFMA
+// tiles, the K loop in k-subs of 32 through a ring of NS stages [A BM x 32 | B BN x 32] (the [rows][32] images of
+// gemm8: 64-byte rows, 16-byte chunk c of row r at c ^ ((-(r >> 2)) & 3), filled by LDS-DMA with the swizzle on the
+// source address).  Stage s + NS - 1 is issued right after the barrier of k-sub s, so NS - 2 stages stay in flight
+// across every barrier (counted vmcnt, never 0 in the loop), and the fragments of stage s + 1 are read into the
+// second register set while the MFMAs of stage s run: the wave's own MFMA stream covers its LDS read latency.
+// One barrier per k-sub.
+//   RAW: stage s + 1 is read in k-sub s, after a wait that leaves only the stages issued after it in flight and the
+//        barrier of k-sub s (every wave's DMA of s + 1 retired before any wave passes it);
+//   WAR: stage s + NS - 1 goes into the slot of stage s - 1, whose fragments every wave read in k-sub s - 2 and
+//        consumed by its MFMAs of k-sub s - 1, before arriving at barrier s.
+// The LDS-DMA of a stage is (BM + BN) / 16 wave instructions (16 rows x 64 B each), dealt round-robin over the
+// waves; a wave's counted waits use its own share (wave-uniform).
+template <int BM, int BN, int NS, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm4r_kernel(GemmArgs g) {
+  constexpr int NT = 256, WN = 2;
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  static_assert(TM * 16 == WTM && TN * 16 == WTN, "wave tile");
+  constexpr int HK = 32;
+  constexpr int A_INS = BM / 16, B_INS = BN / 16, INS = A_INS + B_INS;  // wave instructions per stage (all waves)
+  constexpr int STAGE = (BM + BN) * HK;
+  constexpr int LDC = BN + 8;
+  constexpr int LDS_ELEMS = NS * STAGE > BM * LDC ? NS * STAGE : BM * LDC;
+  static_assert(NS >= 3 && NS <= 6 && LDS_ELEMS * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) f16 lds[LDS_ELEMS];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  int mt, nt;
+  tile_of(wgid, (g.M + BM - 1) / BM, tiles_n, g.xb, mt, nt);
+  const int m0 = mt * BM;
+  const int n0 = nt * BN;
+
+  const int src_chunk = (lane & 3) ^ ((-(lane >> 4)) & 3);
+  const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.A, 0, (int)(((int64_t)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t b_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.B, 0, (int)(((int64_t)(g.N - 1) * g.ldb + g.K) * 2), 0x00020000);
+  // every wave issues WINS instructions per stage: instruction i = wid + 4u (A rows first, then B rows); when 4
+  // does not divide INS the last round repeats instructions of other waves (the same bytes to the same LDS
+  // addresses), so every wave's counted waits are the same compile-time numbers
+  constexpr int WINS = (INS + 3) / 4;
+  int voff[WINS], dsto[WINS];
+  bool isa[WINS];
+#pragma unroll
+  for (int u = 0; u < WINS; ++u) {
+    int i = wid + 4 * u;
+    if (i >= INS) i -= 4;
+    isa[u] = i < A_INS;
+    const int row = (isa[u] ? i : i - A_INS) * 16;
+    const int64_t grow = (int64_t)(isa[u] ? m0 : n0) + row + (lane >> 2);
+    voff[u] = (int)((grow * (isa[u] ? g.lda : g.ldb) + src_chunk * 8) * 2);
+    dsto[u] = (isa[u] ? 0 : BM * HK) + row * HK;
+  }
+  auto issue = [&](int s) {
+    f16* dst = lds + (s % NS) * STAGE;
+    const int kb = s * HK * 2;
+#pragma unroll
+    for (int u = 0; u < WINS; ++u) {
+      // rounds wholly in A or wholly in B need no test; the round straddling them branches (wave-uniform)
+      const bool all_a = (u + 1) * 4 <= A_INS, all_b = u * 4 >= A_INS && B_INS >= 4;
+      if (all_a || (!all_b && isa[u]))
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(dst + dsto[u]), 16, voff[u] + kb, 0, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_ptr_t)(dst + dsto[u]), 16, voff[u] + kb, 0, 0, 0);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fg = lane >> 4;
+  const int frag_off = fr * HK + ((fg ^ ((-(fr >> 2)) & 3)) << 3);
+  auto read = [&](f16x8 (&af)[TM], f16x8 (&bf)[TN], int s) {
+    const f16* img = lds + (s % NS) * STAGE;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = *(const f16x8*)(img + (wm * WTM + i * 16) * HK + frag_off);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bf[j] = *(const f16x8*)(img + BM * HK + (wn * WTN + j * 16) * HK + frag_off);
+  };
+  auto mma = [&](const f16x8 (&af)[TM], const f16x8 (&bf)[TN]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+  };
+
+  const int ns = g.K / HK;  // k-subs; the launcher guarantees ns >= NS
+  MF_STAMP(0);
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue(s);
+  wait_vmcnt<WINS * (NS - 2)>();  // stage 0 landed
+  lds_barrier();
+  f16x8 a0[TM], b0[TN], a1[TM], b1[TN];
+  read(a0, b0, 0);
+  MF_STAMP(1);
+  // steady k-sub s (s + NS - 1 < ns): retire s + 1 (NS - 3 younger stages in flight), barrier, issue s + NS - 1,
+  // read s + 1 into the other register set, MFMAs of s
+  auto steady = [&](int s, f16x8 (&ac)[TM], f16x8 (&bc)[TN], f16x8 (&an)[TM], f16x8 (&bn)[TN]) {
+    wait_vm_lgkm0<WINS * (NS - 3)>();
+    lds_barrier();
+    issue(s + NS - 1);
+    read(an, bn, s + 1);
+    mma(ac, bc);
+  };
+  // the last NS - 1 k-subs: nothing left to issue; the in-flight count falls NS - 3 .. 0
+  auto tail = [&](f16x8 (&a_)[TM], f16x8 (&b_)[TN], f16x8 (&c_)[TM], f16x8 (&d_)[TN]) {
+    const int s0 = ns - (NS - 1);
+#pragma unroll
+    for (int t = 0; t < NS - 1; ++t) {
+      const bool even = (t & 1) == 0;
+      if (t < NS - 2) {
+        if (NS - 3 - t == 3) wait_vm_lgkm0<WINS * 3>();
+        else if (NS - 3 - t == 2) wait_vm_lgkm0<WINS * 2>();
+        else if (NS - 3 - t == 1) wait_vm_lgkm0<WINS * 1>();
+        else wait_vm_lgkm0<0>();
+        lds_barrier();
+        if (even) read(c_, d_, s0 + t + 1);
+        else read(a_, b_, s0 + t + 1);
+      }
+      if (even) mma(a_, b_);
+      else mma(c_, d_);
+    }
+  };
+  const int S0 = ns - (NS - 1);
+  int s = 0;
+  for (; s + 1 < S0; s += 2) {
+    steady(s, a0, b0, a1, b1);
+    steady(s + 1, a1, b1, a0, b0);
+  }
+  if (s < S0) {
+    steady(s, a0, b0, a1, b1);
+    tail(a1, b1, a0, b0);
+  } else {
+    tail(a0, b0, a1, b1);
+  }
+  MF_STAMP(2);
+  __syncthreads();  // every wave is done with the ring (nothing in flight after the last k-sub)
+  epilogue_store<BM, BN, NT, TM, TN, EPI>(g, lds, acc, m0, n0, wm * WTM, wn * WTN, tid, fr, fg);
+  MF_STAMP(3);
+}
+
 // Register-direct epilogue of the persistent kernel: the arithmetic of epilogue_store + epi8 (first rounding
 // fp16(acc + bias) / fp16(acc), then residual / QuickGELU / QuickGELU' in fp32 and one more fp16 rounding),
 // without the LDS staging pass, so the operand ring stays free for the next tile's first K-steps.  A lane's
@@ -1152,6 +1306,25 @@ int launch_tile(const GemmArgs& a, int epi, hipStream_t st) {
   return 0;
 }
 
+template <int BM, int BN, int NS>
+int launch_tile4r(const GemmArgs& a, int epi, hipStream_t st) {
+  if (a.K / 32 < NS) return launch_tile<128, 128, 2, 2, 2>(a, epi, st);  // fewer k-subs than ring stages
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles), block(256);
+  switch (epi) {
+    case EPI_NONE: gemm4r_kernel<BM, BN, NS, EPI_NONE><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS: gemm4r_kernel<BM, BN, NS, EPI_BIAS><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_RESID: gemm4r_kernel<BM, BN, NS, EPI_BIAS_RESID><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_GELU: gemm4r_kernel<BM, BN, NS, EPI_BIAS_GELU><<<grid, block, 0, st>>>(a); break;
+    case EPI_DGELU: gemm4r_kernel<BM, BN, NS, EPI_DGELU><<<grid, block, 0, st>>>(a); break;
+    case EPI_F32: gemm4r_kernel<BM, BN, NS, EPI_F32><<<grid, block, 0, st>>>(a); break;
+    case EPI_RESID: gemm4r_kernel<BM, BN, NS, EPI_RESID><<<grid, block, 0, st>>>(a); break;
+    default: return mf_set_error("mf_gemm_nt: bad epilogue", -2);
+  }
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
 // K-major operand combinations run on the 4-wave kernel's 128x128 / 128x64 / 64x64 tiles (a plain
 // function: kernel templates instantiated only through nested function templates lose their host
 // stubs under hipcc)
@@ -1312,6 +1485,17 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     case 21: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 2, 4>(a, epilogue, st);
     case 22: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 256, 2, 4>(a, epilogue, st);
     case 27: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8sp(a, epilogue, st);
+    // gemm4r: 4 waves, k-sub ring (r04)
+    case 40: return launch_tile4r<256, 256, 4>(a, epilogue, st);
+    case 41: return launch_tile4r<256, 128, 4>(a, epilogue, st);
+    case 43: return launch_tile4r<128, 160, 4>(a, epilogue, st);
+    case 44: return launch_tile4r<160, 128, 4>(a, epilogue, st);
+    case 46: return launch_tile4r<128, 128, 5>(a, epilogue, st);
+    case 48: return launch_tile4r<160, 160, 4>(a, epilogue, st);
+    case 49: return launch_tile4r<128, 192, 4>(a, epilogue, st);
+    case 50: return launch_tile4r<192, 192, 4>(a, epilogue, st);
+    case 51: return launch_tile4r<256, 192, 4>(a, epilogue, st);
+    case 52: return launch_tile4r<192, 128, 4>(a, epilogue, st);
     default: return mf_set_error("mf_gemm: bad tile id", -2);
   }
 }

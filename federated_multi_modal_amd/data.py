@@ -70,10 +70,13 @@ class SyntheticClientDataManager:
     """ClientDataManager stand-in: .train_loader / .test_loader / .num_classes / .lab2cname."""
 
     def __init__(self, client_id: int, classnames: List[str], n_train: int, n_test: int, train_batch: int,
-                 test_batch: int, device, seed: int = 0, image_resolution: int = 224, captions: bool = False):
+                 test_batch: int, device, seed: int = 0, image_resolution: int = 224, captions: bool = False,
+                 unique_images: int = 0):
         """captions: batches carry one synthetic caption string per image (the caption-fork datasets' Datum
         captions), which turns on the caption-conditioned prompts; off, "caption" is None (BASELINE's
-        synthetic configs carry no captions)."""
+        synthetic configs carry no captions).  unique_images > 0: each split generates that many images
+        (rounded up to the 64-image chunk) and repeats them to its size -- the device work per batch is the
+        same, and the host PRNG (~25 ms per image) stays out of long timing runs (bench.py's round wall-time)."""
         self.client_id = client_id
         self._classnames = list(classnames)
         K = len(classnames)
@@ -81,13 +84,18 @@ class SyntheticClientDataManager:
 
         def make(tag: str, n: int) -> _Split:
             imgs, labs = [], []
-            for s0 in range(0, n, 64):  # generate in chunks (host memory)
-                b = syn.client_batch(seed, client_id, zlib.crc32(tag.encode()) + s0, min(64, n - s0), K,
+            n_gen = n if unique_images <= 0 else min(n, unique_images)
+            for s0 in range(0, n_gen, 64):  # generate in chunks (host memory)
+                b = syn.client_batch(seed, client_id, zlib.crc32(tag.encode()) + s0, min(64, n_gen - s0), K,
                                      image_resolution)
                 imgs.append(torch.from_numpy(b.images).to(self.device))
                 labs.append(torch.from_numpy(b.labels).to(self.device))
+            img, lab = torch.cat(imgs), torch.cat(labs)
+            if n_gen < n:
+                reps = (n + n_gen - 1) // n_gen
+                img, lab = img.repeat(reps, 1, 1, 1)[:n].contiguous(), lab.repeat(reps)[:n].contiguous()
             caps = syn.synthetic_captions(seed, client_id, zlib.crc32(tag.encode()), n) if captions else None
-            return _Split(torch.cat(imgs), torch.cat(labs), caps)
+            return _Split(img, lab, caps)
 
         self.train = make("train", n_train)
         self.test = make("test", n_test)

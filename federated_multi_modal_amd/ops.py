@@ -25,17 +25,24 @@ class KernelProbe:
     def __init__(self, kinds="gemm"):
         self.kinds = {kinds} if isinstance(kinds, str) else set(kinds)
         self.kind = next(iter(self.kinds)) if len(self.kinds) == 1 else None  # single-family callers
-        self.records = []  # (key, start_event, end_event, flops, bytes)
+        self.records = []  # (key, start_event, end_event, flops, bytes, meta)
 
     def wants(self, kind: str) -> bool:
         return kind in self.kinds
 
-    def around(self, flops: float, nbytes: float, key: str = "gemm"):
+    def around(self, flops: float, nbytes: float, key: str = "gemm", meta=None):
+        """meta: what the launch was (the GEMMs: (M, N, K, epilogue)), for per-shape tables."""
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
-        self.records.append((key, s, e, flops, nbytes))
+        self.records.append((key, s, e, flops, nbytes, meta))
         return e
+
+    def launches(self):
+        """Per-launch records in launch order: key, duration (us), flops, algorithmic bytes, meta."""
+        torch.cuda.synchronize()
+        return [{"key": k, "us": 1e3 * s.elapsed_time(e), "flops": f, "bytes": b, "meta": m}
+                for k, s, e, f, b, m in self.records]
 
     def keys(self):
         return sorted({r[0] for r in self.records})
@@ -43,7 +50,7 @@ class KernelProbe:
     def summary(self, prefix: Optional[str] = None):
         torch.cuda.synchronize()
         recs = [r for r in self.records if prefix is None or r[0].startswith(prefix)]
-        ms = [s.elapsed_time(e) for _, s, e, _, _ in recs]
+        ms = [r[1].elapsed_time(r[2]) for r in recs]
         n = len(ms)
         tot_ms = sum(ms)
         flops = sum(r[3] for r in recs)
@@ -146,7 +153,7 @@ def gemm_nt(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NON
     ld_aux = _ld(aux) if aux is not None else 0
     ev = None
     if _PROBE is not None and _PROBE.wants("gemm"):
-        ev = _PROBE.around(2.0 * M * N * K, _gemm_bytes(M, N, K, C, aux), _gkey())
+        ev = _PROBE.around(2.0 * M * N * K, _gemm_bytes(M, N, K, C, aux), _gkey(), (M, N, K, epilogue))
     call("mf_gemm_nt", _p(A), _ld(A), _p(B), _ld(B), _p(C), _ld(C), M, N, K, _p(bias), _p(aux_in), _p(aux_out),
          ld_aux, epilogue, tile, _s())
     if ev is not None:
@@ -168,7 +175,7 @@ def gemm(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NONE, 
     ld_aux = _ld(aux) if aux is not None else 0
     ev = None
     if _PROBE is not None and _PROBE.wants("gemm"):
-        ev = _PROBE.around(2.0 * M * N * K, _gemm_bytes(M, N, K, C, aux), _gkey())
+        ev = _PROBE.around(2.0 * M * N * K, _gemm_bytes(M, N, K, C, aux), _gkey(), (M, N, K, epilogue))
     call("mf_gemm", _p(A), _ld(A), int(a_kmajor), _p(B), _ld(B), int(b_kmajor), _p(C), _ld(C), M, N, K, _p(bias),
          _p(aux_in), _p(aux_out), ld_aux, epilogue, tile, _s())
     if ev is not None:
@@ -194,7 +201,7 @@ def gemm_splitk(A, B, C, ws, splits=0, a_kmajor=False, b_kmajor=False):
     assert ws.dtype == torch.float32 and C.dtype in (torch.float16, torch.float32)
     ev = None
     if _PROBE is not None and _PROBE.wants("gemm"):
-        ev = _PROBE.around(2.0 * M * N * K, _gemm_bytes(M, N, K, C), _gkey())
+        ev = _PROBE.around(2.0 * M * N * K, _gemm_bytes(M, N, K, C), _gkey(), (M, N, K, "splitk"))
     call("mf_gemm_splitk", _p(A), _ld(A), int(a_kmajor), _p(B), _ld(B), int(b_kmajor), _p(C), _ld(C), M, N, K,
          _p(ws), ws.numel(), splits, int(C.dtype == torch.float16), _s())
     if ev is not None:
@@ -232,7 +239,7 @@ def gemm_resid_ln(A, W, bias, R, C, gamma, beta, Y, mean, rstd):
     N = W.shape[0]
     ev = None
     if _PROBE is not None and _PROBE.wants("gemm"):
-        ev = _PROBE.around(2.0 * M * N * K, _gemm_bytes(M, N, K, C, R) + 2.0 * M * N + 8.0 * M, _gkey())
+        ev = _PROBE.around(2.0 * M * N * K, _gemm_bytes(M, N, K, C, R) + 2.0 * M * N + 8.0 * M, _gkey(), (M, N, K, "resid_ln"))
     call("mf_gemm_resid_ln", _p(A), _ld(A), _p(W), _ld(W), _p(bias), _p(R), _ld(R), _p(C), _ld(C), _p(gamma),
          _p(beta), _p(Y), _ld(Y), _p(mean), _p(rstd), M, N, K, _s())
     _rec(ev)

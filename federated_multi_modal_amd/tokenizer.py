@@ -59,8 +59,9 @@ def byte_alphabet() -> Dict[int, str]:
     return table
 
 
-# ftfy's uncurl_quotes (U+2018..U+201B -> ', U+201C..U+201F -> ") and fix_latin_ligatures
-_FOLD = {**{chr(c): "'" for c in range(0x2018, 0x201C)}, **{chr(c): '"' for c in range(0x201C, 0x2020)},
+# ftfy's uncurl_quotes (U+02BC and U+2018..U+201B -> ', U+201C..U+201F -> ") and fix_latin_ligatures
+_FOLD = {"\u02bc": "'", **{chr(c): "'" for c in range(0x2018, 0x201C)},
+         **{chr(c): '"' for c in range(0x201C, 0x2020)},
          "\ufb00": "ff", "\ufb01": "fi", "\ufb02": "fl", "\ufb03": "ffi", "\ufb04": "ffl", "\ufb05": "st",
          "\ufb06": "st", "\u0132": "IJ", "\u0133": "ij", "\u01c7": "LJ", "\u01c8": "Lj", "\u01c9": "lj",
          "\u01ca": "NJ", "\u01cb": "Nj", "\u01cc": "nj"}
@@ -80,8 +81,10 @@ def _fix_text_fallback(text: str) -> str:
 try:  # pragma: no cover - not installed in this image
     import ftfy as _ftfy
     _fix_text = _ftfy.fix_text
+    _HAVE_FTFY = True
 except ImportError:
     _fix_text = _fix_text_fallback
+    _HAVE_FTFY = False
 
 
 def clean(text: str) -> str:
@@ -246,6 +249,9 @@ def get_tokenizer(bpe_path: str = "") -> Union[SimpleTokenizer, SyntheticTokeniz
 
 def describe(tok) -> str:
     if tok.kind == "bpe":
-        return f"CLIP byte-level BPE ({tok.path}, {tok.vocab_size} ids)"
+        fix = "ftfy" if _HAVE_FTFY else ("ftfy absent: its quote / ligature / width folds and NFC are applied; its "
+                                         "repairs of broken text (mojibake, control characters, HTML entities "
+                                         "beyond html.unescape) are not, so such captions may tokenize differently")
+        return f"CLIP byte-level BPE ({tok.path}, {tok.vocab_size} ids; {fix})"
     return ("synthetic word ids (no bpe_simple_vocab_16e6.txt.gz found: text features differ from CLIP's "
             "tokenizer on real prompts)")

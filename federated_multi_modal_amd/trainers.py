@@ -24,6 +24,7 @@ from __future__ import annotations
 import dataclasses
 import os
 import os.path as osp
+import time
 from typing import Dict, List, Optional
 
 import torch
@@ -130,6 +131,9 @@ class MaPLe(TrainerX):
             self.device = torch.device(device)
         self.lr_history: List[float] = []
         self.grad_norms: List[float] = []
+        # wall seconds by phase (host clock read at the host syncs run_epoch / test() make anyway): local
+        # training steps, test() passes, and the FedAvg launch hook run between them (MaPLeFederated.round_times)
+        self.timing = {"train_s": 0.0, "test_s": 0.0, "fedavg_launch_s": 0.0, "steps": 0, "epochs": 0}
         self.batch_idx = 0
         self._built = False
         self.check_cfg(cfg)
@@ -310,11 +314,16 @@ class MaPLe(TrainerX):
         self.engine.clear_halt()
         steps = 0
         start = self.total_batches
+        t0 = time.perf_counter()
         for batch_idx, batch in enumerate(self.dm.train_loader):
             self.batch_idx = batch_idx
             self._step_async(batch)
             steps += 1
         bad, ok, bad_in, ok_in = torch.cat([self._bad, self._ok, self._bad_in, self._ok_in]).tolist()
+        t1 = time.perf_counter()  # .tolist() waited for the epoch's last step
+        self.timing["train_s"] += t1 - t0
+        self.timing["steps"] += steps
+        self.timing["epochs"] += 1
         if bad_in != 0.0 and ok_in <= ok:  # check_tensor_validity (trainers/maple.py:556-557): not caught upstream
             self.total_batches = start + int(ok_in) + 1
             self.batch_idx = int(ok_in)
@@ -326,7 +335,10 @@ class MaPLe(TrainerX):
         self.update_lr()
         if before_test is not None:
             before_test()
+        t2 = time.perf_counter()
+        self.timing["fedavg_launch_s"] += t2 - t1
         local = self.test()
+        self.timing["test_s"] += time.perf_counter() - t2  # test() ends in a host read of its counters
         avg_loss = float(self._loss_sum.item()) / max(1, steps)
         print(f"[Client {self.client_id}] Epoch {epoch} done. Loss={avg_loss:.4f}, Acc={local['accuracy']:.2f}%")
         return {"avg_loss": avg_loss}
@@ -449,6 +461,13 @@ def _load_clip_weights(path, cfg, classnames, mcfg, bpe_path=""):
     return engine_state_from_clip(sd, ecfg), dims
 
 
+class _ExchangeLaunchError(BaseException):
+    """The FedAvg collective failed to launch inside a client's epoch hook.  A BaseException, so the per-client
+    handlers of the round loop (which exclude a failed client and exchange again) never see it: the launch is
+    not retried on this rank alone, which would leave its peers in mismatched collectives; train() re-raises
+    the cause."""
+
+
 @TRAINER_REGISTRY.register()
 class MaPLeFederated(TrainerX):
     """The federated aggregator (trainers/maple_fed.py:24-500).
@@ -469,6 +488,7 @@ class MaPLeFederated(TrainerX):
         self.clients: List[MaPLe] = []
         self.global_weights = None
         self.nan_stats = {"total_updates": 0, "failed_clients": [], "skipped_rounds": 0}
+        self.round_times: List[dict] = []  # per round: wall seconds split by phase (train())
         self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         self.rank = dist.get_rank() if self.distributed else 0
         if self.distributed and self.num_clients % dist.get_world_size():
@@ -519,12 +539,15 @@ class MaPLeFederated(TrainerX):
         self.lab2cname = {i: c for i, c in enumerate(names)}
         shots = self.cfg.DATASET.NUM_SHOTS if self.cfg.DATASET.NUM_SHOTS > 0 else 16
         bs = self.cfg.DATALOADER.TRAIN_X.BATCH_SIZE
+        get = self.cfg.FED.get if hasattr(self.cfg.FED, "get") else (lambda k, d: d)
+        n_test, n_unique = get("SYNTHETIC_TEST_IMAGES", 0), get("SYNTHETIC_UNIQUE_IMAGES", 0)
         self.client_data_managers = {}
         for i in self._local_client_ids():
             self.client_data_managers[i] = SyntheticClientDataManager(
-                i, names, n_train=max(bs, min(shots * len(names), 64 * bs)), n_test=self.cfg.DATALOADER.TEST.BATCH_SIZE,
+                i, names, n_train=max(bs, min(shots * len(names), 64 * bs)),
+                n_test=n_test if n_test > 0 else self.cfg.DATALOADER.TEST.BATCH_SIZE,
                 train_batch=bs, test_batch=self.cfg.DATALOADER.TEST.BATCH_SIZE, device=self.device,
-                seed=max(self.cfg.SEED, 0))
+                seed=max(self.cfg.SEED, 0), unique_images=n_unique)
         self.train_loader_x = self.val_loader = self.test_loader = self.dm = None
 
     def build_model(self):
@@ -550,9 +573,21 @@ class MaPLeFederated(TrainerX):
         rank's last client packs, the exchange (federated.FedAvgExchange) is launched there, flies while the
         test batches run, and is waited for after the client loop.  The result equals the reference's
         FedAvg-after-training order: the test reads the same local weights and the bucket holds them.  A
-        client whose test() then raises is still excluded (finish re-exchanges with its vote withdrawn)."""
+        client whose test() then raises is still excluded (finish re-exchanges with its vote withdrawn).
+
+        Each round appends its wall time, split by phase, to self.round_times (the FedAvg round wall-time of
+        SURVEY.md §8(d): local epochs + tests + exchange); bench.py reports it."""
+        try:
+            self._train_rounds()
+        except _ExchangeLaunchError as err:  # a collective that failed to launch is not a client failure
+            raise err.__cause__
+        self.finalize_training()
+
+    def _train_rounds(self):
         for round_idx in range(self.num_rounds):
             print(f"\n--- Federated Round {round_idx + 1}/{self.num_rounds} ---")
+            t_round = time.perf_counter()
+            before = [dict(getattr(c, "timing", {})) for c in self.clients]
             self.broadcast_weights()
             round_losses, late_failed, abort = [], [], None
             n_local = len(self.clients)
@@ -570,9 +605,12 @@ class MaPLeFederated(TrainerX):
 
                 def start_fedavg(fed=fed, started=started, last_local=j == n_local - 1):
                     fed.pack()
+                    started.append(True)  # the bucket is out: from here on a failure is a late one
                     if last_local:
-                        self.exchange.start()
-                    started.append(True)
+                        try:
+                            self.exchange.start()
+                        except Exception as err:  # never retried as a client failure (peers would mismatch)
+                            raise _ExchangeLaunchError() from err
                 try:
                     for ep in range(trainer.epoch, trainer.max_epoch):
                         hook = start_fedavg if ep == trainer.max_epoch - 1 else None
@@ -596,22 +634,43 @@ class MaPLeFederated(TrainerX):
                         self.exchange.start()
             if round_losses:
                 print(f"[Round {round_idx + 1}] Avg local training loss = {sum(round_losses) / len(round_losses):.4f}")
+            t_fin = time.perf_counter()
             try:
                 n_valid = self._fedavg_finish(late_failed, abort=abort is not None)
             except FederatedAbort:
                 if abort is not None:
                     raise abort
                 raise
+            dev = getattr(self, "device", None)
+            if isinstance(dev, torch.device) and dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            t_avg = time.perf_counter()
             if n_valid > 0:
                 self.nan_stats["total_updates"] += 1
             else:
                 print("All clients failed! Reverting to previous global model.")
                 self.nan_stats["skipped_rounds"] += 1
             self.global_weights = self.clients[0].model.state_dict()
+            t_gt = time.perf_counter()
             if self.rank == 0:
                 res = self.clients[0].test()
                 print(f"[Round {round_idx + 1}] Test accuracy (client 0) = {res['accuracy']:.2f}%")
-        self.finalize_training()
+            t_end = time.perf_counter()
+            d = {k: sum(getattr(c, "timing", {}).get(k, 0) - b.get(k, 0) for c, b in zip(self.clients, before))
+                 for k in ("train_s", "test_s", "fedavg_launch_s", "steps", "epochs")}
+            rec = {"round": round_idx + 1, "wall_s": t_end - t_round, "local_train_s": d["train_s"],
+                   "local_test_s": d["test_s"], "fedavg_launch_s": d["fedavg_launch_s"],
+                   # the exchange's wait + unpack after the client loop: what the overlap with the last test() left
+                   "fedavg_exposed_s": t_avg - t_fin,
+                   "global_state_s": t_gt - t_avg, "global_test_s": t_end - t_gt,
+                   "steps": d["steps"], "epochs": d["epochs"], "clients": len(self.clients), "valid": n_valid}
+            # broadcast, LR schedule, prints, loader iteration: the round's host time outside the timed phases
+            rec["other_s"] = rec["wall_s"] - sum(rec[k] for k in ("local_train_s", "local_test_s", "fedavg_launch_s",
+                                                                  "fedavg_exposed_s", "global_state_s",
+                                                                  "global_test_s"))
+            if not hasattr(self, "round_times"):
+                self.round_times = []
+            self.round_times.append(rec)
 
     def _fedavg(self, failed_local) -> int:
         """check_weights_valid + safe_average_weights + broadcast, on the device (federated.py), for

@@ -363,3 +363,41 @@ def test_fused_qkv_attention_does_not_change_results(dev, monkeypatch, handwritt
     assert torch.equal(q0, q1) and torch.equal(o0, o1)
     for n in g0:
         assert torch.equal(g0[n], g1[n]), n
+
+
+@pytest.mark.parametrize("J,K,B", [(9, 38, 32), (9, 1000, 32)], ids=["c4", "c5"])
+def test_graph_replay_equals_eager_step(dev, J, K, B):
+    """The captured step (one hipGraph: the text tower forked onto the side stream and joined back, the
+    optimizer's halt latch, the LR read from device memory) computes exactly what the same step launched
+    eagerly computes, at the bench's C4 shape and at C5 (K = 1 000): two engines built identically take the
+    same eager first step (momentum buffers created), then engine A runs step 2 eagerly and engine B replays
+    its captured graph on the same batch -- loss, every trainable gradient, the updated weights and the
+    momentum, bit for bit.  A missing or misplaced cross-stream edge in the captured graph (r03: forking the
+    text tower ahead of the prompt learner it reads) shows here as a mismatch."""
+    names = syn.synthetic_classnames(K, 0)
+    b0, b1 = syn.client_batch(0, 0, 0, B, K), syn.client_batch(0, 0, 1, B, K)
+    out = []
+    for graph in (False, True):
+        e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=0), device=dev)
+        e.set_lr(0.0026)
+        e.load_batch(torch.from_numpy(b0.images), torch.from_numpy(b0.labels))
+        e.train_step()
+        if graph:
+            g = e.capture_train_step()
+            e.load_batch(torch.from_numpy(b1.images), torch.from_numpy(b1.labels))
+            g.replay()
+        else:
+            e.load_batch(torch.from_numpy(b1.images), torch.from_numpy(b1.labels))
+            e.train_step()
+        torch.cuda.synchronize()
+        out.append({"loss": e.loss_out.detach().clone().cpu(), "gflat16": e.gflat16.detach().clone().cpu(),
+                    "gflat32": e.gflat32.detach().clone().cpu(), "flat16": e.flat16.detach().clone().cpu(),
+                    "flat32": e.flat32.detach().clone().cpu(),
+                    "mom": [e.mom16.detach().clone().cpu(), e.mom32.detach().clone().cpu()]})
+        del e
+        torch.cuda.empty_cache()
+    a, g = out
+    assert torch.isfinite(a["loss"][:1]).all()
+    for k in ("loss", "gflat16", "gflat32", "flat16", "flat32"):
+        assert torch.equal(a[k], g[k]), k
+    assert len(a["mom"]) == len(g["mom"]) > 0 and all(torch.equal(x, y) for x, y in zip(a["mom"], g["mom"]))

@@ -336,3 +336,42 @@ def test_round_loop_abort_stops_every_rank():
     assert res[0][4].startswith("FederatedAbort") and res[2][4].startswith("FederatedAbort")
     for rank in range(3):
         assert res[rank][2]["total_updates"] == 1   # round 0 completed everywhere
+
+
+def test_exchange_launch_failure_is_not_retried_as_a_client_failure():
+    """A FedAvg collective that fails to launch inside the last client's epoch hook propagates out of train()
+    (its cause re-raised) instead of being taken for a client failure: the round loop does not pack the bucket
+    again as 'failed' and does not launch the exchange a second time on this rank alone (which would leave the
+    peers in mismatched collectives).  One process, the exchange replaced by a stub that fails on start()."""
+    from federated_multi_modal_amd.config import extend_cfg, get_cfg_default
+    from federated_multi_modal_amd.federated import FedAvgBucket
+    from federated_multi_modal_amd.trainers import MaPLeFederated
+
+    class FailingExchange:
+        def __init__(self):
+            self.starts = 0
+
+        def start(self):
+            self.starts += 1
+            raise RuntimeError("collective launch failed")
+
+        def finish(self, *a, **k):
+            raise AssertionError("finish() must not run after a failed launch")
+
+    cfg = get_cfg_default()
+    extend_cfg(cfg)
+    tr = MaPLeFederated.__new__(MaPLeFederated)
+    tr.cfg, tr.num_clients, tr.num_rounds, tr.local_epochs = cfg, 1, 2, 2
+    tr.nan_stats = {"total_updates": 0, "failed_clients": [], "skipped_rounds": 0}
+    tr.distributed, tr.rank = False, 0
+    tr.clients = [FakeClient(0)]
+    tr.fed = [FedAvgBucket(tr.clients[0].engine, kernels=HostKernels, mode="ordered")]
+    packs = []
+    orig_pack = tr.fed[0].pack
+    tr.fed[0].pack = lambda failed=False: (packs.append(failed), orig_pack(failed=failed))
+    tr.exchange = FailingExchange()
+    tr.save_model = lambda *a, **k: None
+    with pytest.raises(RuntimeError, match="collective launch failed"):
+        tr.train()
+    assert tr.exchange.starts == 1 and packs == [False]
+    assert tr.nan_stats["failed_clients"] == []
