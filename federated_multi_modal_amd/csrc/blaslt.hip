@@ -1,4 +1,7 @@
-// hipBLASLt for the plain library GEMMs of the step (host code only).
+// hipBLASLt as a yardstick for the hand-written GEMMs (host code only).  OFF by default since r04: every product of
+// the step runs on the hand-written gfx950 kernels of gemm.hip; MAPFED_GEMM_LIB=1 (or mf_gemm_lib_enable) routes
+// the products below to hipBLASLt for A/B runs against the vendor library (tests/diagnostics/gemm_bench.py also
+// times torch.mm, i.e. hipBLASLt, beside every tile).
 //
 // The hand-written kernels (gemm.hip) carry every fused epilogue of the path (residual add, QuickGELU and its
 // derivative at the reference's fp16 rounding points).  Three products have no epilogue beyond a bias and
@@ -44,7 +47,7 @@ struct LibState {
   hipblasLtHandle_t handle = nullptr;
   void* ws = nullptr;
   size_t ws_bytes = 0;
-  int enabled = 1;
+  int enabled = 0;
   std::map<std::tuple<int, int, int, int64_t, int64_t, int64_t, int>, Plan> plans;
 };
 
@@ -63,8 +66,8 @@ extern "C" int mf_gemm_lib_init(void* workspace, int64_t bytes) {
     return mf_set_error("mf_gemm_lib_init: hipblasLtCreate failed", -1);
   s.ws = workspace;
   s.ws_bytes = workspace ? (size_t)bytes : 0;
-  const char* env = getenv("MAPFED_GEMM_LIB");  // A/B knob: 0 keeps every product on the hand-written kernels
-  if (env) s.enabled = atoi(env) != 0;
+  const char* env = getenv("MAPFED_GEMM_LIB");  // A/B knob: 1 routes the products below to hipBLASLt
+  s.enabled = env && atoi(env) != 0;
   return 0;
 }
 

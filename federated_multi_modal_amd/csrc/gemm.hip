@@ -822,189 +822,6 @@ __global__ __launch_bounds__(512) void gemm8s_kernel(GemmArgs g) {
   MF_STAMP(3);
 }
 
-// Instruction order of one k-sub of gemm4r, pinned for the scheduler (cdna_hip_programming.md T19): hipcc otherwise
-// sinks the next stage's fragment reads to just before their first use (one register set live), which puts their
-// latency back in front of the MFMAs.  Each MFMA is followed by one LDS-DMA issue and one fragment read until those
-// run out, so the reads land under the MFMA stream.  Masks: MFMA 0x8, VMEM read 0x20, DS read 0x100.
-template <int NMFMA, int NVMEM, int NDS>
-MF_DEV void sched_ksub() {
-#pragma unroll
-  for (int k = 0; k < NMFMA; ++k) {
-    __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-    if (k < NVMEM) __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
-    if (k < NDS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-  }
-}
-
-// one stage of gemm4r's LDS-DMA: this wave's WINS instructions (rows of A or of B, 16 rows x 64 B each) at byte
-// column kb.  The buffer descriptors are built here from (pointer, byte range), as dma_stage does: a kernel
-// template whose lambdas capture a descriptor can lose its host stub under hipcc.
-template <int WINS, int A_INS, int B_INS>
-MF_DEV void dma4r_stage(const f16* A, int a_bytes, const f16* B, int b_bytes, f16* dst, const int* voff,
-                        const int* dsto, const int* isa, int kb) {
-  const auto a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, a_bytes, 0x00020000);
-  const auto b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, b_bytes, 0x00020000);
-#pragma unroll
-  for (int u = 0; u < WINS; ++u) {
-    // rounds wholly in A or wholly in B need no test; the round straddling them branches (wave-uniform)
-    const bool all_a = (u + 1) * 4 <= A_INS, all_b = u * 4 >= A_INS && B_INS >= 4;
-    if (all_a || (!all_b && isa[u]))
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(dst + dsto[u]), 16, voff[u] + kb, 0, 0, 0);
-    else
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_ptr_t)(dst + dsto[u]), 16, voff[u] + kb, 0, 0, 0);
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// gemm4r: BM x BN tile on 4 waves (2 x 2, one wave per SIMD), each wave a (BM/2) x (BN/2) block of 16x16 MFMA
-// tiles.  The K loop runs in stages of KS k-subs of 32 through a ring of NS stages; a stage holds KS image pairs
-// [A BM x 32 | B BN x 32] (the [rows][32] images of gemm8: 64-byte rows, 16-byte chunk c of row r at
-// c ^ ((-(r >> 2)) & 3), filled by LDS-DMA with the swizzle on the source address).  Stage s + NS - 1 is issued right
-// after the barrier of stage s, so NS - 2 stages stay in flight across every barrier (counted vmcnt, never 0 in the
-// loop).  The MFMAs of k-sub j run while the fragments of k-sub j + 1 are read into the other register set -- for
-// the last k-sub of a stage, the first k-sub of stage s + 1, which the wait before barrier s already retired -- so
-// the wave's own MFMA stream covers its LDS read latency.  One barrier per stage.
-//   RAW: stage s + 1 is first read in stage s, after a wait that leaves only the stages issued after it in flight
-//        and the barrier of stage s (every wave's DMA of s + 1 retired before any wave passes it);
-//   WAR: stage s + NS - 1 goes into the slot of stage s - 1, whose last reads every wave issued in stage s - 1 and
-//        consumed by its MFMAs there, before arriving at barrier s.
-// The LDS-DMA of one k-sub is (BM + BN) / 16 wave instructions (16 rows x 64 B each), dealt round-robin over the
-// waves.  Tiles up to 160 x 160 stay within 256 VGPRs (no accumulator moves through AGPRs); larger ones get the
-// 512-register file of one wave per SIMD.
-template <int BM, int BN, int NS, int KS, int EPI>
-__global__ __launch_bounds__(256, (BM * BN <= 160 * 160) ? 2 : 1) void gemm4r_kernel(GemmArgs g) {
-  constexpr int NT = 256, WN = 2;
-  constexpr int WTM = BM / 2, WTN = BN / 2;
-  constexpr int TM = WTM / 16, TN = WTN / 16;
-  static_assert(TM * 16 == WTM && TN * 16 == WTN, "wave tile");
-  static_assert(KS == 2 || KS == 4, "k-subs per stage (even: every stage starts on register set 0)");
-  constexpr int HK = 32;
-  constexpr int A_INS = BM / 16, B_INS = BN / 16, INS = A_INS + B_INS;  // wave instructions per k-sub (all waves)
-  constexpr int SUB = (BM + BN) * HK;
-  constexpr int STAGE = KS * SUB;
-  constexpr int LDC = BN + 8;
-  constexpr int LDS_ELEMS = NS * STAGE > BM * LDC ? NS * STAGE : BM * LDC;
-  static_assert(NS >= 3 && NS <= 6 && LDS_ELEMS * 2 <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(1024))) f16 lds[LDS_ELEMS];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WN, wn = wid % WN;
-  const int tiles_n = (g.N + BN - 1) / BN;
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  int mt, nt;
-  tile_of(wgid, (g.M + BM - 1) / BM, tiles_n, g.xb, mt, nt);
-  const int m0 = mt * BM;
-  const int n0 = nt * BN;
-
-  const int src_chunk = (lane & 3) ^ ((-(lane >> 4)) & 3);
-  const int a_bytes = (int)(((int64_t)(g.M - 1) * g.lda + g.K) * 2);
-  const int b_bytes = (int)(((int64_t)(g.N - 1) * g.ldb + g.K) * 2);
-  // every wave issues WINS instructions per k-sub: instruction i = wid + 4u (A rows first, then B rows); when 4
-  // does not divide INS the last round repeats instructions of other waves (the same bytes to the same LDS
-  // addresses), so every wave's counted waits are the same compile-time numbers
-  constexpr int WINS = (INS + 3) / 4;
-  constexpr int SINS = WINS * KS;  // per wave per stage
-  int voff[WINS], dsto[WINS], isa[WINS];
-#pragma unroll
-  for (int u = 0; u < WINS; ++u) {
-    int i = wid + 4 * u;
-    if (i >= INS) i -= 4;
-    isa[u] = i < A_INS;
-    const int row = (isa[u] ? i : i - A_INS) * 16;
-    const int64_t grow = (int64_t)(isa[u] ? m0 : n0) + row + (lane >> 2);
-    voff[u] = (int)((grow * (isa[u] ? g.lda : g.ldb) + src_chunk * 8) * 2);
-    dsto[u] = (isa[u] ? 0 : BM * HK) + row * HK;
-  }
-  auto issue = [&](int s) {
-#pragma unroll
-    for (int j = 0; j < KS; ++j)
-      dma4r_stage<WINS, A_INS, B_INS>(g.A, a_bytes, g.B, b_bytes, lds + (s % NS) * STAGE + j * SUB, voff, dsto, isa,
-                                      (s * KS + j) * HK * 2);
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int fr = lane & 15, fg = lane >> 4;
-  const int frag_off = fr * HK + ((fg ^ ((-(fr >> 2)) & 3)) << 3);
-  auto read = [&](f16x8 (&af)[TM], f16x8 (&bf)[TN], int s, int j) {
-    const f16* img = lds + (s % NS) * STAGE + j * SUB;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) af[i] = *(const f16x8*)(img + (wm * WTM + i * 16) * HK + frag_off);
-#pragma unroll
-    for (int jj = 0; jj < TN; ++jj) bf[jj] = *(const f16x8*)(img + BM * HK + (wn * WTN + jj * 16) * HK + frag_off);
-  };
-  auto mma = [&](const f16x8 (&af)[TM], const f16x8 (&bf)[TN]) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
-  };
-
-  const int nst = g.K / (HK * KS);  // stages; the launcher guarantees K % (32 KS) == 0 and nst >= NS
-  MF_STAMP(0);
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s) issue(s);
-  wait_vmcnt<SINS * (NS - 2)>();  // stage 0 landed
-  lds_barrier();
-  f16x8 a0[TM], b0[TN], a1[TM], b1[TN];
-  read(a0, b0, 0, 0);
-  MF_STAMP(1);
-  // the k-subs of stage s (its barrier passed); last: no stage after it
-  auto body = [&](int s, bool last, bool issued) {
-#pragma unroll
-    for (int j = 0; j < KS; ++j) {
-      const bool even = (j & 1) == 0;
-      if (j + 1 < KS) {
-        if (even) read(a1, b1, s, j + 1);
-        else read(a0, b0, s, j + 1);
-      } else if (!last) {
-        read(a0, b0, s + 1, 0);  // KS even: the next stage starts on set 0
-      }
-      if (even) mma(a0, b0);
-      else mma(a1, b1);
-      if (j == 0 && issued) sched_ksub<TM * TN, SINS, TM + TN>();
-      else sched_ksub<TM * TN, 0, TM + TN>();
-    }
-  };
-  const int S0 = nst - (NS - 1);
-  for (int s = 0; s < S0; ++s) {
-    __builtin_amdgcn_sched_barrier(0);
-    wait_vm_lgkm0<SINS * (NS - 3)>();  // stage s + 1 landed (NS - 3 younger stages in flight)
-    lds_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    issue(s + NS - 1);
-    body(s, false, true);
-  }
-  // the last NS - 1 stages: nothing left to issue; the in-flight count falls NS - 3 .. 0
-#pragma unroll
-  for (int t = 0; t < NS - 1; ++t) {
-    const int s = S0 + t;
-    if (t < NS - 2) {
-      __builtin_amdgcn_sched_barrier(0);
-      if (NS - 3 - t == 3) wait_vm_lgkm0<SINS * 3>();
-      else if (NS - 3 - t == 2) wait_vm_lgkm0<SINS * 2>();
-      else if (NS - 3 - t == 1) wait_vm_lgkm0<SINS * 1>();
-      else wait_vm_lgkm0<0>();
-      lds_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    body(s, t == NS - 2, false);
-  }
-  MF_STAMP(2);
-  __syncthreads();  // every wave is done with the ring (nothing in flight after the last stage)
-  epilogue_store<BM, BN, NT, TM, TN, EPI>(g, lds, acc, m0, n0, wm * WTM, wn * WTN, tid, fr, fg);
-  MF_STAMP(3);
-}
-
 // Register-direct epilogue of the persistent kernel: the arithmetic of epilogue_store + epi8 (first rounding
 // fp16(acc + bias) / fp16(acc), then residual / QuickGELU / QuickGELU' in fp32 and one more fp16 rounding),
 // without the LDS staging pass, so the operand ring stays free for the next tile's first K-steps.  A lane's
@@ -1335,25 +1152,6 @@ int launch_tile(const GemmArgs& a, int epi, hipStream_t st) {
   return 0;
 }
 
-template <int BM, int BN, int NS, int KS>
-int launch_tile4r(const GemmArgs& a, int epi, hipStream_t st) {
-  if (a.K % (32 * KS) || a.K / (32 * KS) < NS) return launch_tile<128, 128, 2, 2, 2>(a, epi, st);  // short / odd K
-  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  dim3 grid(tiles), block(256);
-  switch (epi) {
-    case EPI_NONE: gemm4r_kernel<BM, BN, NS, KS, EPI_NONE><<<grid, block, 0, st>>>(a); break;
-    case EPI_BIAS: gemm4r_kernel<BM, BN, NS, KS, EPI_BIAS><<<grid, block, 0, st>>>(a); break;
-    case EPI_BIAS_RESID: gemm4r_kernel<BM, BN, NS, KS, EPI_BIAS_RESID><<<grid, block, 0, st>>>(a); break;
-    case EPI_BIAS_GELU: gemm4r_kernel<BM, BN, NS, KS, EPI_BIAS_GELU><<<grid, block, 0, st>>>(a); break;
-    case EPI_DGELU: gemm4r_kernel<BM, BN, NS, KS, EPI_DGELU><<<grid, block, 0, st>>>(a); break;
-    case EPI_F32: gemm4r_kernel<BM, BN, NS, KS, EPI_F32><<<grid, block, 0, st>>>(a); break;
-    case EPI_RESID: gemm4r_kernel<BM, BN, NS, KS, EPI_RESID><<<grid, block, 0, st>>>(a); break;
-    default: return mf_set_error("mf_gemm_nt: bad epilogue", -2);
-  }
-  MF_CHECK_LAUNCH();
-  return 0;
-}
-
 // K-major operand combinations run on the 4-wave kernel's 128x128 / 128x64 / 64x64 tiles (a plain
 // function: kernel templates instantiated only through nested function templates lose their host
 // stubs under hipcc)
@@ -1514,15 +1312,6 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     case 21: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 2, 4>(a, epilogue, st);
     case 22: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 256, 2, 4>(a, epilogue, st);
     case 27: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8sp(a, epilogue, st);
-    // gemm4r: 4 waves, ring of 2-k-sub stages (r04)
-    case 70: return launch_tile4r<160, 128, 4, 2>(a, epilogue, st);
-    case 71: return launch_tile4r<128, 160, 4, 2>(a, epilogue, st);
-    case 72: return launch_tile4r<256, 128, 3, 2>(a, epilogue, st);
-    case 73: return launch_tile4r<128, 128, 4, 2>(a, epilogue, st);
-    case 75: return launch_tile4r<160, 128, 3, 2>(a, epilogue, st);
-    case 77: return launch_tile4r<192, 128, 4, 2>(a, epilogue, st);
-    case 78: return launch_tile4r<128, 192, 4, 2>(a, epilogue, st);
-    case 79: return launch_tile4r<160, 160, 3, 2>(a, epilogue, st);
     default: return mf_set_error("mf_gemm: bad tile id", -2);
   }
 }

@@ -433,7 +433,8 @@ class MapleEngine:
         size, same model), as trainers/maple.py:660-681 evaluates the model being trained."""
         self.cfg = cfg
         self.device = torch.device(device)
-        ops.gemm_lib_init(self.device)  # hipBLASLt for the plain products it runs faster (csrc/blaslt.hip)
+        if ops.gemm_lib_default():  # MAPFED_GEMM_LIB=1: the hipBLASLt yardstick route (csrc/blaslt.hip), A/B only
+            ops.gemm_lib_init(self.device)
         self.tokenizer = get_tokenizer(cfg.bpe_path)  # prompts and captions (CLIP BPE or the synthetic ids)
         d = cfg.dims
         self.B, self.K, self.J = cfg.batch, len(cfg.classnames), cfg.prompt_depth

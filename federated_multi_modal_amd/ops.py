@@ -7,6 +7,7 @@ passes preallocated buffers so a whole step can be captured in a hipGraph).
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -124,9 +125,15 @@ GEMM_LIB_WS_BYTES = 64 << 20
 _LIB_WS: Optional[torch.Tensor] = None
 
 
+def gemm_lib_default() -> bool:
+    """The hipBLASLt route is an A/B yardstick, off unless MAPFED_GEMM_LIB=1 (csrc/blaslt.hip)."""
+    return os.environ.get("MAPFED_GEMM_LIB", "0") not in ("", "0")
+
+
 def gemm_lib_init(device) -> None:
     """Create the hipBLASLt handle and hand it a workspace that outlives every captured graph (idempotent);
-    from then on mf_gemm's heuristic tile path routes the products mf_gemm_lib_wants() names to hipBLASLt."""
+    with the route enabled (MAPFED_GEMM_LIB=1 or gemm_lib_enable(True)) mf_gemm's heuristic tile path sends the
+    products mf_gemm_lib_wants() names to hipBLASLt."""
     global _LIB_WS
     if _LIB_WS is None:
         _LIB_WS = torch.empty(GEMM_LIB_WS_BYTES, dtype=torch.uint8, device=device)

@@ -2,6 +2,7 @@
 reference of the same op.  Tolerances are written per test; fp16 outputs are compared in units of
 the fp16 ulp of the reference value."""
 import math
+import os
 
 import pytest
 import torch
@@ -738,6 +739,7 @@ def test_gemm_lib_route(dev, M, N, K, epi):
     Against float64 like every GEMM kernel, deterministic, and bit-identical to the hand-written kernel on the
     same operands (measured on MI355X for every shape here: the route changes no result of the step)."""
     ops.gemm_lib_init(dev)
+    assert not ops.gemm_lib_default() or os.environ.get("MAPFED_GEMM_LIB")  # off unless asked for (r04)
     g = torch.Generator(device="cpu").manual_seed(M + 7 * N + K)
     A = torch.randn(M, K, generator=g).half().to(dev)
     B = (torch.randn(N, K, generator=g) * K ** -0.5).half().to(dev)
@@ -752,12 +754,14 @@ def test_gemm_lib_route(dev, M, N, K, epi):
              ops._p(b), epi, ops._s())
     assert torch.equal(C, C2)  # deterministic
     ops.gemm_lib_enable(False)
-    try:
-        H = ops.gemm_nt(A, B, bias=b, epilogue=epi)
-    finally:
-        ops.gemm_lib_enable(True)
+    H = ops.gemm_nt(A, B, bias=b, epilogue=epi)
     d = int((C.view(torch.int16).int() - H.view(torch.int16).int()).abs().max())
     print(f"{M}x{N}x{K} epi {epi}: hipBLASLt vs hand-written: bit-identical {torch.equal(C, H)}, max {d} ulp")
     assert torch.equal(C, H)
     if M >= 2048:
-        assert ops.gemm_lib_wants(M, N, K, epi)
+        assert not ops.gemm_lib_wants(M, N, K, epi)  # the route is off: the step runs the hand-written kernels
+        ops.gemm_lib_enable(True)
+        try:
+            assert ops.gemm_lib_wants(M, N, K, epi)
+        finally:
+            ops.gemm_lib_enable(ops.gemm_lib_default())
