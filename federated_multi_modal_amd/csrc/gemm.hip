@@ -1280,9 +1280,10 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     if (t256 >= 192 && t256 <= 256 && K >= 512)
       tile = gemm_rule() == 3 ? 22 : 20;  // one round of 256x256 tiles on one workgroup per CU (vision QKV: 225 tiles), gemm8s
     else if (M >= 16384 && K >= 512)  // the C5 text tower (M = 77 000): many rounds of tiles whatever the
-      // shape, so the tile's own efficiency decides (gemm_bench.py ... c5): 256x256 for N >= 2048, 160x128
+      // shape, so the tile's own efficiency decides (gemm_bench.py ... c5): 256x256 for N >= 1536 (r04: the
+      // in-projection N = 1536 746 against 678 TFLOP/s on 160x128, profiles/r04_v3_c5_gemm_tiles.txt), 160x128
       // otherwise (+6..40 % over the M = 6368 picks on the N = 512 products)
-      tile = N >= 2048 ? 20 : 10;
+      tile = N >= 1536 ? 20 : 10;
     else if (M >= 4096 && K >= 512)  // vision products (M = 6368), tests/diagnostics/gemm_bench.py:
       // N = 3072: 160x128 (960 tiles); N = 768: 96x128 (402 tiles, two workgroups per CU) for K >= 2048,
       // 160x64 (480 tiles) for K = 768; +6..37 % over the 128-row tiles
