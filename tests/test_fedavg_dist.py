@@ -269,7 +269,7 @@ def _train_worker(rank, world, port, per_rank, fail, late, abort, out):
         err = f"{type(exc).__name__}: {exc}"
     out[rank] = ([(c.engine.flat16.clone(), c.engine.flat32.clone()) for c in tr.clients],
                  [list(c.events) for c in tr.clients], dict(tr.nan_stats),
-                 [c.engine.momentum_resets for c in tr.clients], err)
+                 [c.engine.momentum_resets for c in tr.clients], err, list(getattr(tr, "round_times", [])))
     dist.destroy_process_group()
 
 
@@ -306,8 +306,14 @@ def test_round_loop_distributed(world, per_rank, fail, late):
             avg = O.safe_average_weights(locals_)
             g16, g32 = avg["a"], avg["b"].float()
     for rank in range(world):
-        weights, events, stats, resets, err = res[rank]
+        weights, events, stats, resets, err, rounds = res[rank]
         assert err is None, err
+        # MaPLeFederated.round_times: one record per round, its phases inside the round's wall time
+        assert [r["round"] for r in rounds] == [1, 2]
+        for r in rounds:
+            parts = sum(r[k] for k in ("local_train_s", "local_test_s", "fedavg_launch_s", "fedavg_exposed_s",
+                                       "global_state_s", "global_test_s", "other_s"))
+            assert abs(parts - r["wall_s"]) < 1e-6 and r["wall_s"] >= 0.0 and r["clients"] == per_rank
         for j, (p16, p32) in enumerate(weights):
             c = rank * per_rank + j
             assert torch.equal(p16, g16) and torch.equal(p32, g32), c
