@@ -1,5 +1,7 @@
 """Diagnostic (GPU box): a few launches of one GEMM tile on one shape, for rocprofv3 --pmc passes:
-    python gemm_one.py M N K tile [reps]"""
+    python gemm_one.py M N K tile [reps] [epi]
+tile 0 with MAPFED_GEMM_LIB=1 and a product the yardstick route takes (e.g. 6368 2304 768 0 4 1: the vision
+in-projection with its bias) runs hipBLASLt's kernel instead, for a counter-by-counter comparison."""
 import sys
 from pathlib import Path
 
@@ -10,12 +12,16 @@ from federated_multi_modal_amd import ops  # noqa: E402
 
 M, N, K, tile = (int(x) for x in sys.argv[1:5])
 reps = int(sys.argv[5]) if len(sys.argv) > 5 else 5
+epi = int(sys.argv[6]) if len(sys.argv) > 6 else ops.EPI_NONE
 dev = torch.device("cuda:0")
 torch.manual_seed(0)
 A = torch.randn(M, K, device=dev).half()
 B = (torch.randn(N, K, device=dev) * K ** -0.5).half()
 C = torch.empty(M, N, device=dev, dtype=torch.float16)
+bias = (torch.randn(N, device=dev) * 0.1).half() if epi == ops.EPI_BIAS else None
+if ops.gemm_lib_default():
+    ops.gemm_lib_init(dev)
 for _ in range(reps):
-    ops.gemm_nt(A, B, C=C, epilogue=ops.EPI_NONE, tile=tile)
+    ops.gemm_nt(A, B, C=C, bias=bias, epilogue=epi, tile=tile)
 torch.cuda.synchronize()
 print("ok", M, N, K, tile)
