@@ -46,8 +46,6 @@ struct GemmArgs {
   int ksplit;  // > 0: split-K slice of ksplit (multiple of 64) per slice z, fp32 partial at C + z*M*ldc
   int xb;      // log2 of the N-range count of the XCD blocking (tile_of); 0: M-ranges only; split-K: 1 =
                // N-major positions inside a slice (split_tile_of)
-  int nt = 0;  // 1: C (and the QuickGELU' output) stored non-temporally -- outputs far larger than the L2s and the
-               // Infinity Cache (the C5 text tower's 236-315 MB planes), which a cached store only churns
 };
 
 // The QuickGELU pre-activation (EPI_BIAS_GELU's aux output) is read again only by the backward, so it is
@@ -138,8 +136,7 @@ MF_DEV void epi8(const GemmArgs& g, int64_t m, int n, int cnt, const f16* t, f16
 #pragma unroll
       for (int e = 0; e < 8; ++e) out[e] = (f16)quick_gelu16_bwd((float)tv[e], (float)aux[e]);
     }
-    if (g.nt) st16_stream(crow, out);
-    else *(f16x8*)crow = out;
+    *(f16x8*)crow = out;
     return;
   }
   for (int e = 0; e < cnt; ++e) {
@@ -1193,15 +1190,6 @@ inline int text_tile() {
   return t;
 }
 
-// Non-temporal C stores for outputs of more than 128 MB (MAPFED_GEMM_NT: 0 never, 1 that rule (default), 2 always;
-// A/B knob).  Such a plane (the C5 text tower's in-projection, c_fc and c_proj-dX outputs, 236-315 MB) is far larger
-// than the eight 4 MB L2s and the 256 MB Infinity Cache, so caching its lines only evicts the operand panels the
-// running tiles re-read.
-inline int gemm_nt_store(int M, int N) {
-  static const int mode = getenv("MAPFED_GEMM_NT") ? atoi(getenv("MAPFED_GEMM_NT")) : 1;
-  return mode == 2 || (mode == 1 && (int64_t)M * N * 2 > (128LL << 20));
-}
-
 // XCD blocking (tile_of): the N-range count 2^xb minimising one XCD's operand footprint A/(8/2^xb) +
 // B/2^xb (bytes of the A rows and B rows it reads); MAPFED_GEMM_XB overrides (A/B knob, -1 = auto)
 inline int gemm_xcd_split(int M, int N, int K) {
@@ -1275,7 +1263,6 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
                    (!aux_in || (uintptr_t)aux_in % 16 == 0) && (!aux_out || (uintptr_t)aux_out % 16 == 0);
   GemmArgs a{(const f16*)A, (const f16*)B, C, (const f16*)bias, (const f16*)aux_in, (f16*)aux_out,
              lda, ldb, ldc, ld_aux, M, N, K, vec8, 0, gemm_xcd_split(M, N, K)};
-  a.nt = gemm_nt_store(M, N);
   hipStream_t st = (hipStream_t)stream;
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   if (a_kmajor || b_kmajor) {
