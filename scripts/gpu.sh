@@ -16,6 +16,13 @@
 #   digest     tests/diagnostics/step_digest.py $DIGEST_CFGS (bit-identity A/B of two trees: compare the lines)
 #   ab         interleaved bench A/B of env knobs: VARIANTS="A=1 B=2,C=3 -" ROUNDS times (scripts/bench_ab.sh)
 #   attn       tests/diagnostics/attn_bench.py $ATTN_ARGS
+#   pmc_bench  FETCH / WRITE / MFMA-busy passes over a short bench run (scripts/gpu_pmc.sh -> gpurun_out/pmc_summary.json)
+#   pmc_attn   PMC passes over the attention kernels (scripts/attn_pmc.sh -> gpurun_out/attn_pmc_summary.json)
+#   pmc_probe  stall / LDS / MFMA counter passes over single GEMM launches (scripts/gemm_pmc_probe.sh; CONFIGS, LIB)
+#   stamps_gemm / stamps_attn / stamps_qkv   in-kernel timelines (scripts/{gemm,attn,qkv}_stamps.sh; SHAPES)
+#   ab_c5      interleaved C5 A/B of env knobs (scripts/ab_c5.sh; VARIANTS, ROUNDS)
+# Two-tree A/B (scripts/make_ab.sh REV, then scripts/ab_dirs.sh / ab_digest.sh) and ab_gemm_dirs.sh stay separate:
+# they need a second build of the library prepared on the CPU side first.
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
@@ -79,6 +86,13 @@ step() {
       timeout -k 10 300 python3 -u tests/diagnostics/attn_bench.py ${ATTN_ARGS:-} > gpurun_out/attn_bench.txt 2>&1
       rc=$?; echo "attn rc=$rc"; grep -v amdgpu.ids gpurun_out/attn_bench.txt | tail -40
       return $rc ;;
+    pmc_bench) bash scripts/gpu_pmc.sh; return $? ;;
+    pmc_attn) bash scripts/attn_pmc.sh; return $? ;;
+    pmc_probe) bash scripts/gemm_pmc_probe.sh; return $? ;;
+    stamps_gemm) bash scripts/gemm_stamps.sh; return $? ;;
+    stamps_attn) bash scripts/attn_stamps.sh; return $? ;;
+    stamps_qkv) bash scripts/qkv_stamps.sh; return $? ;;
+    ab_c5) bash scripts/ab_c5.sh; return $? ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
 }
