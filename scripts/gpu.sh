@@ -86,8 +86,10 @@ step() {
       timeout -k 10 300 python3 -u tests/diagnostics/attn_bench.py ${ATTN_ARGS:-} > gpurun_out/attn_bench.txt 2>&1
       rc=$?; echo "attn rc=$rc"; grep -v amdgpu.ids gpurun_out/attn_bench.txt | tail -40
       return $rc ;;
-    pmc_bench) bash scripts/gpu_pmc.sh; return $? ;;
-    pmc_attn) bash scripts/attn_pmc.sh; return $? ;;
+    pmc_bench)  # the per-dispatch CSVs are large: only the summary is kept
+      BENCH_ARGS="$QUICK ${BENCH_ARGS:-}" bash scripts/gpu_pmc.sh; rc=$?
+      rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_mfma; return $rc ;;
+    pmc_attn) bash scripts/attn_pmc.sh; rc=$?; rm -rf gpurun_out/apmc_*/; return $rc ;;
     pmc_probe) bash scripts/gemm_pmc_probe.sh; return $? ;;
     stamps_gemm) bash scripts/gemm_stamps.sh; return $? ;;
     stamps_attn) bash scripts/attn_stamps.sh; return $? ;;
