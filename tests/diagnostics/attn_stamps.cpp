@@ -40,6 +40,17 @@ int main(int argc, char** argv) {
     if (rc) { printf("error %s\n", mf_last_error()); return 1; }
     hipDeviceSynchronize();
   }
+  if (fwd) {  // output checksum (bit patterns of O, LSE): variants that claim bit-identity print the same numbers
+    std::vector<short> ho((size_t)R * D);
+    std::vector<float> hl((size_t)NH * L);
+    hipMemcpy(ho.data(), o, ho.size() * 2, hipMemcpyDeviceToHost);
+    hipMemcpy(hl.data(), lse, hl.size() * 4, hipMemcpyDeviceToHost);
+    long long co = 0;
+    double cl = 0;
+    for (short v : ho) co += v;
+    for (float v : hl) cl += v;
+    printf("checksum O %lld LSE %.9g\n", co, cl);
+  }
   if (fwd && getenv("STAMP_FWD4")) {  // attn_fwd4_kernel: every workgroup, id = x * qsplit + y
     const int qs = atoi(getenv("STAMP_FWD4"));
     const int nwg = NH * qs;
