@@ -1292,10 +1292,19 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
       tile = N >= 2048 ? 15 : 26;  // text (M = 2926): c_fc and its dX on 96x128, QKV on 96x64
     else if (M >= 2048 && N <= 768 && K >= 512 && gemm_rule() != 1 && gemm_rule() != 2)
       tile = 26;  // text N = 512 products (out-proj, c_proj, their dX, dQKV): 96x64, 248 tiles, +5..20 % over 64x64
-    else
+    else if (M < 2048 && K >= 512) {
+      // the small clients' products (C2 / C3: B = 4 images, 796 rows; K = 10 classes, 770 rows), r04 sweep
+      // (gemm_bench.py ... c3, profiles/r04_v12_gemm_c3_tiles.txt): the long-K products run few tiles whose
+      // K loops are latency-bound, so a 4-stage ring (64x64, or 32x64 when 64x64 gives < 128 tiles) is
+      // +40..57 % (c_proj / c_fc dX / QKV dX); the wide ones take 96x64 (vision c_fc and its dX, text QKV)
+      const int64_t t64 = (int64_t)((M + 63) / 64) * ((N + 63) / 64);
+      if (K >= 2048) tile = t64 >= 128 ? 31 : 33;
+      else if (N >= 3072 || (N > 1024 && N < 2048)) tile = 26;
+      else tile = 3;
+    } else
       tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
   }
-  // tile ids: the ones the heuristic picks (1, 2, 3, 10, 15, 16, 20 = gemm8s, 26), plus 11 (160x128 with a
+  // tile ids: the ones the heuristic picks (1, 2, 3, 10, 15, 16, 20 = gemm8s, 26, 31, 33), plus 11 (160x128 with a
   // 3-stage ring), 21 (8-wave 256x128) and 22 (the unstaggered gemm8 at 256x256) as A/B baselines
   // (tests/diagnostics/gemm_bench.py); the
   // sweep also covered 128x192, 192x128, 128x160, 160x160, 224x128, 96x192, 64x128, 160x192, 192x192,
@@ -1309,6 +1318,8 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     case 15: return launch_tile<96, 128, 2, 2, 2>(a, epilogue, st);
     case 16: return launch_tile<160, 64, 2, 2, 2>(a, epilogue, st);
     case 26: return launch_tile<96, 64, 2, 2, 2>(a, epilogue, st);
+    case 31: return launch_tile<64, 64, 2, 2, 4>(a, epilogue, st);
+    case 33: return launch_tile<32, 64, 2, 2, 4>(a, epilogue, st);
     case 20: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8s(a, epilogue, st);
     case 21: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 2, 4>(a, epilogue, st);
     case 22: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 256, 2, 4>(a, epilogue, st);

@@ -6,6 +6,7 @@ each tile configuration against a torch fp32 matmul.  Prints TFLOP/s.
                                         big: square 4096^3 / 8192^3 products instead of the step's shapes
                                         (the guide's long-K yardstick for the main loop alone);
                                         c5: the K = 1000 text tower's products (77 000 rows)
+                                        c3: the B = 4 / K = 10 client's products (796 / 770 rows)
 
 A "!" marks a tile whose plain product misses the fp32 reference, "~" one whose output (with the
 shape's epilogue) is not bit-identical to the first listed tile's.
@@ -68,6 +69,15 @@ def main():
                   ("c5.proj", 77000, 512, 2048, ops.EPI_BIAS_RESID, 12),
                   ("c5.dfc", 77000, 2048, 512, ops.EPI_DGELU, 12), ("c5.dh", 77000, 512, 2048, ops.EPI_NONE, 12),
                   ("c5.do", 77000, 512, 512, ops.EPI_NONE, 12), ("c5.dqkv", 77000, 512, 1536, ops.EPI_NONE, 12)]
+    if len(sys.argv) > 2 and sys.argv[2] == "c3":  # C3 / C2 clients: B = 4 images (4 x 199 rows), K = 10 classes
+        shapes = [("c3v.qkv", 796, 2304, 768, ops.EPI_BIAS, 12), ("c3v.out", 796, 768, 768, ops.EPI_BIAS_RESID, 12),
+                  ("c3v.fc", 796, 3072, 768, ops.EPI_BIAS_GELU, 12), ("c3v.proj", 796, 768, 3072, ops.EPI_BIAS_RESID, 12),
+                  ("c3v.dfc", 796, 3072, 768, ops.EPI_DGELU, 12), ("c3v.dh", 796, 768, 3072, ops.EPI_NONE, 12),
+                  ("c3v.do", 796, 768, 768, ops.EPI_NONE, 12), ("c3v.dqkv", 796, 768, 2304, ops.EPI_NONE, 12),
+                  ("c3t.qkv", 770, 1536, 512, ops.EPI_BIAS, 12), ("c3t.out", 770, 512, 512, ops.EPI_BIAS_RESID, 12),
+                  ("c3t.fc", 770, 2048, 512, ops.EPI_BIAS_GELU, 12), ("c3t.proj", 770, 512, 2048, ops.EPI_BIAS_RESID, 12),
+                  ("c3t.dfc", 770, 2048, 512, ops.EPI_DGELU, 12), ("c3t.dh", 770, 512, 2048, ops.EPI_NONE, 12),
+                  ("c3t.do", 770, 512, 512, ops.EPI_NONE, 12), ("c3t.dqkv", 770, 512, 1536, ops.EPI_NONE, 12)]
     if len(sys.argv) > 2 and sys.argv[2] == "big":
         shapes = [("4096^3", 4096, 4096, 4096, ops.EPI_NONE, 1), ("8192^3", 8192, 8192, 8192, ops.EPI_NONE, 1),
                   ("v.fc K4k", 6368, 3072, 4096, ops.EPI_NONE, 1), ("v.qkv K3k", 6368, 2304, 3072, ops.EPI_NONE, 1)]
