@@ -1296,9 +1296,9 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
       // the small clients' products (C2 / C3: B = 4 images, 796 rows; K = 10 classes, 770 rows), r04 sweep
       // (gemm_bench.py ... c3, profiles/r04_v12_gemm_c3_tiles.txt): the long-K products run few tiles whose
       // K loops are latency-bound, so a 4-stage ring (64x64, or 32x64 when 64x64 gives < 128 tiles) is
-      // +40..57 % (c_proj / c_fc dX / QKV dX); the wide ones take 96x64 (vision c_fc and its dX, text QKV)
+      // +8..57 % (c_proj / c_fc dX / QKV dX); the wide ones take 96x64 (vision c_fc and its dX, text QKV)
       const int64_t t64 = (int64_t)((M + 63) / 64) * ((N + 63) / 64);
-      if (K >= 2048) tile = t64 >= 128 ? 31 : 33;
+      if (K >= 1536) tile = t64 >= 128 ? 31 : 33;
       else if (N >= 3072 || (N > 1024 && N < 2048)) tile = 26;
       else tile = 3;
     } else

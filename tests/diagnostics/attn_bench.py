@@ -32,7 +32,7 @@ def timeit(fn, it=20):
 
 
 dev = torch.device("cuda:0")
-for (N, L, H, causal) in [(32, 199, 12, False), (38, 77, 8, True), (4, 199, 12, False), (32, 263, 12, False),
+for (N, L, H, causal) in [(32, 199, 12, False), (38, 77, 8, True), (4, 199, 12, False), (10, 77, 8, True), (32, 263, 12, False),
                              (32, 455, 12, False), (1000, 77, 8, True)]:
     D = H * 64
     torch.manual_seed(L + N)
