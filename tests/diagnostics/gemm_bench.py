@@ -7,6 +7,7 @@ each tile configuration against a torch fp32 matmul.  Prints TFLOP/s.
                                         (the guide's long-K yardstick for the main loop alone);
                                         c5: the K = 1000 text tower's products (77 000 rows)
                                         c3: the B = 4 / K = 10 client's products (796 / 770 rows)
+                                        eval: a 100-image test batch's forward products (19 900 rows)
 
 A "!" marks a tile whose plain product misses the fp32 reference, "~" one whose output (with the
 shape's epilogue) is not bit-identical to the first listed tile's.
@@ -78,6 +79,9 @@ def main():
                   ("c3t.fc", 770, 2048, 512, ops.EPI_BIAS_GELU, 12), ("c3t.proj", 770, 512, 2048, ops.EPI_BIAS_RESID, 12),
                   ("c3t.dfc", 770, 2048, 512, ops.EPI_DGELU, 12), ("c3t.dh", 770, 512, 2048, ops.EPI_NONE, 12),
                   ("c3t.do", 770, 512, 512, ops.EPI_NONE, 12), ("c3t.dqkv", 770, 512, 1536, ops.EPI_NONE, 12)]
+    if len(sys.argv) > 2 and sys.argv[2] == "eval":  # test() batches: 100 images (19 900 rows), forward only
+        shapes = [("ev.qkv", 19900, 2304, 768, ops.EPI_BIAS, 12), ("ev.out", 19900, 768, 768, ops.EPI_BIAS_RESID, 12),
+                  ("ev.fc", 19900, 3072, 768, ops.EPI_BIAS_GELU, 12), ("ev.proj", 19900, 768, 3072, ops.EPI_BIAS_RESID, 12)]
     if len(sys.argv) > 2 and sys.argv[2] == "big":
         shapes = [("4096^3", 4096, 4096, 4096, ops.EPI_NONE, 1), ("8192^3", 8192, 8192, 8192, ops.EPI_NONE, 1),
                   ("v.fc K4k", 6368, 3072, 4096, ops.EPI_NONE, 1), ("v.qkv K3k", 6368, 2304, 3072, ops.EPI_NONE, 1)]
