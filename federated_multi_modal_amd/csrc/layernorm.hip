@@ -273,8 +273,12 @@ __global__ __launch_bounds__(256) void ln_fwd2_kernel(const f16* __restrict__ x,
   }
 }
 
-template <int D>
-__global__ __launch_bounds__(256) void ln_bwd2_kernel(const f16* __restrict__ dy, int64_t lddy,
+// HWB half-waves per 16-row block: 8 (two rows each) or, for few blocks (the small clients' 796 / 770 rows, ~50
+// blocks), 16 (one row each: twice the waves in flight per row block).  The partials stay bit-identical: a pair of
+// one-row half-waves is summed first (fl(a + b) = fl(b + a), and 0 + a is exact), which is what a two-row
+// half-wave's accumulator holds, then the 8 pair sums in order.
+template <int D, int HWB = 8>
+__global__ __launch_bounds__(HWB * 32) void ln_bwd2_kernel(const f16* __restrict__ dy, int64_t lddy,
                                                      const f16* __restrict__ x, int64_t ldx,
                                                      const int* __restrict__ ridx, const float* __restrict__ gamma,
                                                      const float* __restrict__ mean_in,
@@ -284,9 +288,10 @@ __global__ __launch_bounds__(256) void ln_bwd2_kernel(const f16* __restrict__ dy
                                                      int rows, float* __restrict__ inj_part = nullptr,
                                                      int inj_L = 1, int inj_row0 = 0, int inj_n = 0) {
   constexpr int CH = D / 256;
-  constexpr int RPH = LN_ROWS_PER_BLOCK / 8;  // rows per half-wave
-  __shared__ float red_g[8][D];
-  __shared__ float red_b[8][D];
+  static_assert(HWB == 8 || HWB == 16, "half-waves per block");
+  constexpr int RPH = LN_ROWS_PER_BLOCK / HWB;  // rows per half-wave
+  __shared__ float red_g[HWB][D];
+  __shared__ float red_b[HWB][D];
   const int hl = threadIdx.x & 31;
   const int hw = threadIdx.x >> 5;
   float gv[CH * 8];
@@ -373,7 +378,7 @@ __global__ __launch_bounds__(256) void ln_bwd2_kernel(const f16* __restrict__ dy
       }
     }
   }
-  // the 8 half-waves' column partials through LDS (fixed order: deterministic)
+  // the half-waves' column partials through LDS (fixed order: deterministic)
 #pragma unroll
   for (int j = 0; j < CH; ++j)
 #pragma unroll
@@ -382,12 +387,17 @@ __global__ __launch_bounds__(256) void ln_bwd2_kernel(const f16* __restrict__ dy
       red_b[hw][8 * (hl + 32 * j) + e] = accb[j * 8 + e];
     }
   __syncthreads();
-  for (int col = threadIdx.x; col < D; col += 256) {
+  for (int col = threadIdx.x; col < D; col += HWB * 32) {
     float sg = 0.f, sb = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      sg += red_g[k][col];
-      sb += red_b[k][col];
+      if constexpr (HWB == 16) {
+        sg += red_g[2 * k][col] + red_g[2 * k + 1][col];
+        sb += red_b[2 * k][col] + red_b[2 * k + 1][col];
+      } else {
+        sg += red_g[k][col];
+        sb += red_b[k][col];
+      }
     }
     dg_part[(int64_t)blockIdx.x * D + col] = sg;
     db_part[(int64_t)blockIdx.x * D + col] = sb;
@@ -400,6 +410,15 @@ __global__ __launch_bounds__(256) void ln_bwd2_kernel(const f16* __restrict__ dy
 inline int ln_text_rph() {
   static const int r = getenv("MAPFED_LN_TEXT_RPH") ? atoi(getenv("MAPFED_LN_TEXT_RPH")) : 1;
   return r == 2 || r == 4 ? r : 1;
+}
+
+// one row per half-wave (16 half-waves per row block) when the row blocks alone cannot fill the chip: below 256
+// blocks (the c4 text tower's 183, the small clients' ~50; tests/diagnostics/ln_bench.py, r04: 8.43 -> 7.58 us at
+// 2 926 x 512, 8.11 -> 7.43 at 796 x 768; at 6 368 x 768, 398 blocks, 14.3 -> 15.7, so not there).
+// MAPFED_LN_BWD_WIDE=0 / 1 forces the 8 / 16 half-wave form (A/B knob)
+inline bool ln_bwd_wide(int nblk) {
+  static const int w = getenv("MAPFED_LN_BWD_WIDE") ? atoi(getenv("MAPFED_LN_BWD_WIDE")) : -1;
+  return w < 0 ? nblk < 256 : w != 0;
 }
 
 inline int ln_variant() {
@@ -457,9 +476,15 @@ extern "C" int mf_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int
                    (!dres || ((uintptr_t)dres % 16 == 0 && ldres % 8 == 0)) && lddy % 8 == 0 && ldx % 8 == 0 &&
                    lddx % 8 == 0;
   if (ln_variant() == 2 && v16) {
-    if (D == 768)
+    if (D == 768 && ln_bwd_wide(nblk))
+      ln_bwd2_kernel<768, 16><<<nblk, 512, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, row_index, gamma, mean,
+                                                    rstd, (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows);
+    else if (D == 768)
       ln_bwd2_kernel<768><<<nblk, 256, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, row_index, gamma, mean, rstd,
                                                 (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows);
+    else if (ln_bwd_wide(nblk))
+      ln_bwd2_kernel<512, 16><<<nblk, 512, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, row_index, gamma, mean,
+                                                    rstd, (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows);
     else
       ln_bwd2_kernel<512><<<nblk, 256, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, row_index, gamma, mean, rstd,
                                                 (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows);
@@ -579,10 +604,18 @@ extern "C" int mf_layernorm_bwd_inject(const void* dy, int64_t lddy, const void*
   float* dg_part = workspace;
   float* db_part = workspace + (int64_t)nblk * D;
   hipStream_t st = (hipStream_t)stream;
-  if (D == 768)
+  if (D == 768 && ln_bwd_wide(nblk))
+    ln_bwd2_kernel<768, 16><<<nblk, 512, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, nullptr, gamma, mean, rstd,
+                                                  (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows,
+                                                  inj_part, L, row0, nrows);
+  else if (D == 768)
     ln_bwd2_kernel<768><<<nblk, 256, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, nullptr, gamma, mean, rstd,
                                               (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows, inj_part,
                                               L, row0, nrows);
+  else if (ln_bwd_wide(nblk))
+    ln_bwd2_kernel<512, 16><<<nblk, 512, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, nullptr, gamma, mean, rstd,
+                                                  (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows,
+                                                  inj_part, L, row0, nrows);
   else
     ln_bwd2_kernel<512><<<nblk, 256, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, nullptr, gamma, mean, rstd,
                                               (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows, inj_part,
