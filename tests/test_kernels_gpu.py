@@ -127,7 +127,10 @@ def test_gemm_side_tower_tile_hint_is_bit_identical(dev, M, N, K, epi):
                                         (170, 260, 192, 11),
                                         # 96x128, 160x64, 96x64 (tiles 15, 16, 26) as chosen by the heuristic
                                         (6368, 768, 3072, 0), (6368, 768, 768, 0), (2926, 1536, 512, 0),
-                                        (97, 200, 64, 15), (161, 72, 128, 16), (100, 76, 192, 26)])
+                                        (97, 200, 64, 15), (161, 72, 128, 16), (100, 76, 192, 26),
+                                        # the small clients' 4-stage rings (tiles 31, 33)
+                                        (796, 768, 3072, 31), (770, 512, 2048, 33), (100, 72, 320, 31),
+                                        (33, 136, 192, 33)])
 def test_gemm_bias(dev, M, N, K, tile):
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g).half().to(dev)
