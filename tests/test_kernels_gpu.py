@@ -3,6 +3,7 @@ reference of the same op.  Tolerances are written per test; fp16 outputs are com
 the fp16 ulp of the reference value."""
 import math
 import os
+from pathlib import Path
 
 import pytest
 import torch
@@ -768,3 +769,46 @@ def test_gemm_lib_route(dev, M, N, K, epi):
             assert ops.gemm_lib_wants(M, N, K, epi)
         finally:
             ops.gemm_lib_enable(ops.gemm_lib_default())
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(796, 768, 3072, 2), (796, 768, 2304, 0), (770, 512, 2048, 2),
+                                       (770, 512, 1536, 0), (796, 3072, 768, 3), (770, 1536, 512, 1)])
+def test_small_client_tiles_bit_identical(dev, M, N, K, epi):
+    """The small clients' tile picks (4-stage 64x64 / 32x64 rings, 96x64; csrc/gemm.hip) keep the K order of the
+    64x64 two-stage tile they replaced: outputs (and the pre-activation of the QuickGELU epilogue) bit-identical."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + epi)
+    A = torch.randn(M, K, generator=g).half().to(dev)
+    B = (torch.randn(N, K, generator=g) * K ** -0.5).half().to(dev)
+    kw = {}
+    if epi in (ops.EPI_BIAS, ops.EPI_BIAS_RESID, ops.EPI_BIAS_GELU):
+        kw["bias"] = (torch.randn(N, generator=g) * 0.1).half().to(dev)
+    if epi == ops.EPI_BIAS_RESID:
+        kw["aux_in"] = torch.randn(M, N, generator=g).half().to(dev)
+    outs = []
+    for tile in (0, 3):
+        aux_out = torch.empty(M, N, device=dev, dtype=torch.float16) if epi == ops.EPI_BIAS_GELU else None
+        outs.append((ops.gemm_nt(A, B, aux_out=aux_out, epilogue=epi, tile=tile, **kw), aux_out))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if epi == ops.EPI_BIAS_GELU:
+        assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_layernorm_bwd_forms_bit_identical(tmp_path):
+    """The LayerNorm backward with one row per half-wave (chosen below 256 row blocks) and the two-rows form give
+    bit-identical dx, dgamma and dbeta.  The form is read once per process (MAPFED_LN_BWD_WIDE), so each runs in
+    a child process (tests/diagnostics/ln_bwd_dump.py) and the saved outputs are compared here."""
+    import subprocess
+    import sys
+    import numpy as np
+    root = Path(__file__).resolve().parents[1]
+    outs = []
+    for wide in ("0", "1"):
+        f = tmp_path / f"ln_{wide}.npz"
+        env = dict(os.environ, MAPFED_LN_BWD_WIDE=wide)
+        res = subprocess.run([sys.executable, str(root / "tests/diagnostics/ln_bwd_dump.py"), str(f)], cwd=root, env=env,
+                             stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+        assert res.returncode == 0, res.stdout[-2000:]
+        outs.append(dict(np.load(f)))
+    assert outs[0].keys() == outs[1].keys()
+    for k in outs[0]:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
