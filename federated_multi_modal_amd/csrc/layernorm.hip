@@ -273,8 +273,8 @@ __global__ __launch_bounds__(256) void ln_fwd2_kernel(const f16* __restrict__ x,
   }
 }
 
-// HWB half-waves per 16-row block: 8 (two rows each) or, for few blocks (the small clients' 796 / 770 rows, ~50
-// blocks), 16 (one row each: twice the waves in flight per row block).  The partials stay bit-identical: a pair of
+// HWB half-waves per 16-row block: 8 (two rows each) or, for few blocks (ln_bwd_wide: below 256, i.e. the c4 text
+// tower and the small clients), 16 (one row each: twice the waves in flight per row block).  The partials stay bit-identical: a pair of
 // one-row half-waves is summed first (fl(a + b) = fl(b + a), and 0 + a is exact), which is what a two-row
 // half-wave's accumulator holds, then the 8 pair sums in order.
 template <int D, int HWB = 8>
