@@ -340,17 +340,21 @@ def test_c5_full_size_properties(dev):
 
 
 def test_fused_qkv_attention_does_not_change_results(dev, monkeypatch, handwritten_gemm):
-    """The in-projection + attention forward as one launch (MAPFED_FUSED_QKV_ATTN=1, opt-in) against the
-    unfused pair on the hand-written GEMM: logits, loss and every gradient bit-identical at the c4 client
-    shape (J = 9, K = 38, B = 32)."""
+    """The in-projection + attention forward as one launch against the unfused pair on the hand-written GEMM:
+    both towers fused (MAPFED_FUSED_QKV_ATTN=1), and the default ("side": the text tower, which runs beside the
+    vision tower at c4): logits, loss and every gradient bit-identical at the c4 client shape (J = 9, K = 38,
+    B = 32)."""
     J, K, B, seed = 9, 38, 32, 2
     names = syn.synthetic_classnames(K, seed)
     b = syn.client_batch(seed, 0, 0, B, K)
     out = []
-    for fused in ("0", "1"):
-        monkeypatch.setenv("MAPFED_FUSED_QKV_ATTN", fused)
+    for fused in ("0", "1", None):
+        if fused is None:
+            monkeypatch.delenv("MAPFED_FUSED_QKV_ATTN", raising=False)
+        else:
+            monkeypatch.setenv("MAPFED_FUSED_QKV_ATTN", fused)
         e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed), device=dev)
-        assert e.vis.fused_qkv_attn == (fused == "1") and e.txt.fused_qkv_attn == (fused == "1")
+        assert e.vis.fused_qkv_attn == (fused == "1") and e.txt.fused_qkv_attn == (fused != "0")
         e.load_batch(torch.from_numpy(b.images), torch.from_numpy(b.labels))
         logits = e.forward().clone()
         e.forward_backward()
@@ -358,11 +362,12 @@ def test_fused_qkv_attention_does_not_change_results(dev, monkeypatch, handwritt
                     e.vis.QKV[3].clone(), e.txt.O[5].clone()))
         del e
         torch.cuda.empty_cache()
-    (lg0, l0, g0, q0, o0), (lg1, l1, g1, q1, o1) = out
-    assert torch.equal(lg0, lg1) and l0 == l1
-    assert torch.equal(q0, q1) and torch.equal(o0, o1)
-    for n in g0:
-        assert torch.equal(g0[n], g1[n]), n
+    (lg0, l0, g0, q0, o0) = out[0]
+    for lg1, l1, g1, q1, o1 in out[1:]:
+        assert torch.equal(lg0, lg1) and l0 == l1
+        assert torch.equal(q0, q1) and torch.equal(o0, o1)
+        for n in g0:
+            assert torch.equal(g0[n], g1[n]), n
 
 
 @pytest.mark.parametrize("J,K,B", [(9, 38, 32), (9, 1000, 32)], ids=["c4", "c5"])
