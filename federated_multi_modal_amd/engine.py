@@ -36,8 +36,9 @@ from .tokenizer import get_tokenizer
 F16, F32 = torch.float16, torch.float32
 N_CTX = 2
 # towers whose in-projection + attention forward run as one launch (MAPFED_FUSED_QKV_ATTN overrides: "1" both, "0"
-# neither, "vision" / "text" one); the default "side" fuses the text tower when it runs beside the vision tower on
-# its throughput tiles (c4: tile -1, >= 2 048 rows), chosen by the same-box A/Bs in DESIGN.md §6
+# neither, "vision" / "text" one); the default "side" fuses the tower that runs beside the other one on its
+# throughput tiles (tile -1, >= 2 048 rows: the text tower at c4, the vision tower at C5), chosen by the same-box
+# A/Bs in DESIGN.md §4
 FUSED_QKV_ATTN_DEFAULT = "side"
 
 
@@ -487,8 +488,10 @@ class MapleEngine:
             txt_work = self.txt.N * self.txt.L * self.txt.D ** 2
             (self.txt if txt_work <= vis_work else self.vis).tile = -1
         if os.environ.get("MAPFED_FUSED_QKV_ATTN", FUSED_QKV_ATTN_DEFAULT) == "side":
-            # the text tower's fused in-projection + attention when it is the side tower (c4; r04 A/B, §6)
-            self.txt.fused_qkv_attn = self.txt.tile == -1 and self.txt.Rs[0] >= 2048
+            # the side tower's in-projection + attention as one launch (the text tower at c4, the vision tower at
+            # C5; r04 same-box A/Bs)
+            for t in (self.vis, self.txt):
+                t.fused_qkv_attn = t.tile == -1 and t.Rs[0] >= 2048
         self.side = torch.cuda.Stream(device=self.device)
         self.overlap_towers = True  # False: both towers on the current stream (isolated kernel timing)
         # enqueue (and capture) order of the two towers after the fork: the vision tower (the step's critical
