@@ -551,10 +551,20 @@ def main():
         return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
 
     pmc = sorted((ROOT / "profiles").glob(f"*_{args.config}_gemm_traffic.json"), key=_ver)
+    traffic_note = "no traffic file for this config under profiles/"
     if pmc and args.roofline_kernel == "gemm":
         try:
             tj = json.loads(pmc[-1].read_text())
-            traffic, traffic_alg = tj["traffic_bytes_per_launch"], tj["algorithmic_bytes_per_launch"]
+            t_launches, t_alg = tj["launches"], tj["algorithmic_bytes_per_launch"]
+            # the file must describe THIS probe's launch set: the same launch count over the two probed steps and
+            # the same algorithmic bytes per launch (within 1 %); otherwise its traffic is another kernel set's
+            if t_launches == ps["launches"] and abs(t_alg / ps["bytes_per_launch"] - 1.0) <= 0.01:
+                traffic, traffic_alg = tj["traffic_bytes_per_launch"], t_alg
+                traffic_note = "PMC passes over exactly the launches this probe times"
+            else:
+                traffic_note = (f"{pmc[-1].name} covers {t_launches} launches at {t_alg / 1e6:.2f} MB algorithmic per "
+                                f"launch, this probe {ps['launches']} at {ps['bytes_per_launch'] / 1e6:.2f} MB: stale, "
+                                f"not used")
             traffic_src = str(pmc[-1].relative_to(ROOT))
         except (OSError, ValueError, KeyError):
             traffic = traffic_alg = None
@@ -564,7 +574,8 @@ def main():
     if args.roofline_kernel == "gemm":
         roof = {"bound": "mfma", "achieved": ps["tflops"], "peak": MFMA_PEAK_F16 / 1e12, "unit": "TFLOP/s",
                 "frac": ps["tflops"] * 1e12 / MFMA_PEAK_F16, "traffic": traffic, "traffic_unit": "bytes/launch",
-                "traffic_source": traffic_src, "algorithmic_bytes_per_launch": ps["bytes_per_launch"],
+                "traffic_source": traffic_src, "traffic_note": traffic_note,
+                "algorithmic_bytes_per_launch": ps["bytes_per_launch"],
                 "traffic_source_algorithmic_bytes_per_launch": traffic_alg,
                 "traffic_over_algorithmic": traffic / traffic_alg if traffic and traffic_alg else None,
                 "kernel": "GEMM family: the hand-written gemm_nt_kernel / gemm8(s)_kernel launches (csrc/gemm.hip) -- "

@@ -822,6 +822,169 @@ __global__ __launch_bounds__(512) void gemm8s_kernel(GemmArgs g) {
   MF_STAMP(3);
 }
 
+// gemm8f: the 256x256 8-wave staggered tile of gemm8s with FULL-LINE operand images.  gemm8s stages
+// [256 rows][32 k] half-tiles, so each LDS-DMA wave instruction covers 16 rows x 64 B: half of 16 cache lines,
+// each line fetched twice per K-tile (once per k-sub) -- its TA address/command FIFOs run full 4x as often as
+// hipBLASLt's (r04 PMC).  Here a half-tile is 128 rows x the whole K-tile ([128][64] fp16, 128-B rows, 16-B chunk
+// c of row r at c ^ (r & 7): the 4-wave kernel's conflict-free image), so an instruction covers 8 whole lines
+// (cdna_hip_programming.md §5 "The 256² 8-phase template": 128-row halves of A and B, BK = 64).  Half-tiles of
+// K-tile t, in issue order: H = 4t + {0: B rows 0-127, 1: B rows 128-255, 2: A rows 0-127, 3: A rows 128-255};
+// wave (wm, wn) reads A half wm and B half wn >> 1.  Phases (m-half, k-sub) as gemm8s, so every accumulator sums
+// its k-subs in ascending order: bit-identical to gemm8s and to the 4-wave tiles.  Ring of NSLOT = 10 half-tile
+// slots (160 KiB), half-tile H issued in the memory section of phase H - E (E = 6), K-tile t+1's four half-tiles
+// retired (vmcnt(2 half-tiles), then the barrier) in the memory section of phase 4t + 3.  Hazards under the
+// one-barrier stagger (row 1 runs a barrier behind row 0; row r's memory section of phase P lies between barrier
+// instances 2P + r and 2P + r + 1, its reads complete before instance 2P + r + 2):
+//   RAW: both rows' waits for K-tile t precede instance 8t, the first read of row 0 follows it;
+//   WAR: B halves are last read in phase 4t + 2 (both rows), A0 in 4t + 3 (row 0), A1 in 4t + 3 (row 1); the slot
+//        of H = 4t + h held H - 10 (h = 0, 1: A0 / A1 of t - 3; h = 2, 3: B0 / B1 of t - 2), refilled in phase
+//        H - 6 >= (last read) + 2 in every case (h = 2 tight: B0 of t - 2 last read 4t - 6, refilled 4t - 4).
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm8f_kernel(GemmArgs g) {
+  constexpr int BM = 256, BN = 256, WN = 4, NT = 512;
+  constexpr int WTM = 128, WTN = 64, QTM = 4, TN = 4, TM = 8;
+  constexpr int HALF = 128 * BK;  // fp16 elements per half-tile image
+  constexpr int NSLOT = 10, E = 6;
+  constexpr int LDC = BN + 8;
+  constexpr int LDS_ELEMS = NSLOT * HALF > BM * LDC ? NSLOT * HALF : BM * LDC;
+  static_assert(LDS_ELEMS * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) f16 lds[LDS_ELEMS];
+
+  MF_STAMP(0);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  int mt, nt;
+  tile_of(wgid, (g.M + BM - 1) / BM, tiles_n, g.xb, mt, nt);
+  const int m0 = mt * BM;
+  const int n0 = nt * BN;
+
+  // LDS-DMA: a wave instruction fills 8 rows x 128 B; lane l -> row l >> 3, chunk (l & 7) whose source chunk is
+  // pre-swizzled; wave w fills rows (2w + i) * 8 .. + 7 (i = 0, 1) of every half-tile
+  const int lrow = lane >> 3, schunk = (lane & 7) ^ lrow;
+  const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.A, 0, (int)(((int64_t)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t b_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.B, 0, (int)(((int64_t)(g.N - 1) * g.ldb + g.K) * 2), 0x00020000);
+  const int a_voff = (lrow * (int)g.lda + schunk * 8) * 2;
+  const int b_voff = (lrow * (int)g.ldb + schunk * 8) * 2;
+  auto slot = [&](int h) { return lds + (h % NSLOT) * HALF; };
+  auto issue = [&](int H) {
+    f16* dst = slot(H);
+    const int kofs = (H >> 2) * BK;
+    const int hh = H & 3;
+    if (hh < 2) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = (wid * 2 + i) * 8;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            b_rsrc, (lds_ptr_t)(dst + row * BK), 16,
+            b_voff + (int)(((int64_t)(n0 + hh * 128 + row) * g.ldb + kofs) * 2), 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = (wid * 2 + i) * 8;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            a_rsrc, (lds_ptr_t)(dst + row * BK), 16,
+            a_voff + (int)(((int64_t)(m0 + (hh - 2) * 128 + row) * g.lda + kofs) * 2), 0, 0, 0);
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fg = lane >> 4;
+  // fragment (row fr of a 16-row block, k 8fg .. 8fg + 7 of k-sub s) of a [128][64] image
+  const int foff0 = fr * BK + ((fg ^ (fr & 7)) << 3);
+  const int foff1 = fr * BK + (((4 + fg) ^ (fr & 7)) << 3);
+  const int a_row0 = 0, b_row0 = (wn & 1) * WTN;
+  auto read_a = [&](f16x8 (&af)[QTM], const f16* img, int mh, int foff) {
+#pragma unroll
+    for (int i = 0; i < QTM; ++i) af[i] = *(const f16x8*)(img + (a_row0 + mh * 64 + i * 16) * BK + foff);
+  };
+  auto read_b = [&](f16x8 (&bf)[TN], const f16* img, int foff) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bf[j] = *(const f16x8*)(img + (b_row0 + j * 16) * BK + foff);
+  };
+  auto mma = [&](const f16x8 (&af)[QTM], const f16x8 (&bf)[TN], int mh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < QTM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[mh * QTM + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[mh * QTM + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = g.K / BK;  // >= 2
+  // prologue: half-tiles 0 .. 5; retire K-tile 0 (0 .. 3)
+#pragma unroll
+  for (int h = 0; h < E; ++h) issue(h);
+  wait_vmcnt<2 * 2>();
+  lds_barrier();
+  MF_STAMP(1);
+  if (wm == 1) lds_barrier();  // the stagger
+  f16x8 fx[QTM], fy[QTM], fb0[TN], fb1[TN];
+
+  // one K-tile; MODE 0: steady (issues 4t+6 .. 4t+9, retires K-tile t+1 with two half-tiles in flight),
+  // 1: t = nk-2 (issues 4t+6, 4t+7 = the last two, retires K-tile t+1 with nothing in flight), 2: t = nk-1.
+  auto ktile = [&](int kt, auto mode_tag) {
+    constexpr int MODE = decltype(mode_tag)::value;
+    const int h0 = 4 * kt;
+    const f16* ia = slot(h0 + 2 + wm);
+    const f16* ib = slot(h0 + (wn >> 1));
+    // phase 0 (m-half 0, k-sub 0)
+    read_a(fx, ia, 0, foff0);
+    read_b(fb0, ib, foff0);
+    if constexpr (MODE <= 1) issue(h0 + E);
+    lds_barrier();
+    mma(fx, fb0, 0);
+    lds_barrier();
+    // phase 1 (m-half 1, k-sub 0)
+    read_a(fy, ia, 1, foff0);
+    if constexpr (MODE <= 1) issue(h0 + E + 1);
+    lds_barrier();
+    mma(fy, fb0, 1);
+    lds_barrier();
+    // phase 2 (m-half 1, k-sub 1)
+    read_a(fx, ia, 1, foff1);
+    read_b(fb1, ib, foff1);
+    if constexpr (MODE == 0) issue(h0 + E + 2);
+    lds_barrier();
+    mma(fx, fb1, 1);
+    lds_barrier();
+    // phase 3 (m-half 0, k-sub 1); retire the next K-tile
+    read_a(fy, ia, 0, foff1);
+    if constexpr (MODE == 0) {
+      issue(h0 + E + 3);
+      wait_vmcnt<2 * 2>();
+    } else if constexpr (MODE == 1) {
+      wait_vmcnt<0>();
+    }
+    lds_barrier();
+    mma(fy, fb1, 0);
+    lds_barrier();
+  };
+  for (int kt = 0; kt < nk - 2; ++kt) ktile(kt, std::integral_constant<int, 0>{});
+  ktile(nk - 2, std::integral_constant<int, 1>{});
+  ktile(nk - 1, std::integral_constant<int, 2>{});
+  if (wm == 0) lds_barrier();  // even out the barrier count
+  __syncthreads();
+  MF_STAMP(2);
+  epilogue_store<BM, BN, NT, TM, TN, EPI>(g, lds, acc, m0, n0, wm * WTM, wn * WTN, tid, fr, fg);
+  MF_STAMP(3);
+}
+
 // Register-direct epilogue of the persistent kernel: the arithmetic of epilogue_store + epi8 (first rounding
 // fp16(acc + bias) / fp16(acc), then residual / QuickGELU / QuickGELU' in fp32 and one more fp16 rounding),
 // without the LDS staging pass, so the operand ring stays free for the next tile's first K-steps.  A lane's
@@ -1115,6 +1278,23 @@ int launch_tile8s(const GemmArgs& a, int epi, hipStream_t st) {
   return 0;
 }
 
+int launch_tile8f(const GemmArgs& a, int epi, hipStream_t st) {
+  const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  dim3 grid(tiles), block(512);
+  switch (epi) {
+    case EPI_NONE: gemm8f_kernel<EPI_NONE><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS: gemm8f_kernel<EPI_BIAS><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_RESID: gemm8f_kernel<EPI_BIAS_RESID><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_GELU: gemm8f_kernel<EPI_BIAS_GELU><<<grid, block, 0, st>>>(a); break;
+    case EPI_DGELU: gemm8f_kernel<EPI_DGELU><<<grid, block, 0, st>>>(a); break;
+    case EPI_F32: gemm8f_kernel<EPI_F32><<<grid, block, 0, st>>>(a); break;
+    case EPI_RESID: gemm8f_kernel<EPI_RESID><<<grid, block, 0, st>>>(a); break;
+    default: return mf_set_error("mf_gemm_nt: bad epilogue", -2);
+  }
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int BM, int BN, int WM, int WN>
 int launch_tile8(const GemmArgs& a, int epi, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
@@ -1323,6 +1503,7 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     case 20: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8s(a, epilogue, st);
     case 21: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 2, 4>(a, epilogue, st);
     case 22: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 256, 2, 4>(a, epilogue, st);
+    case 40: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8f(a, epilogue, st);
     case 27: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8sp(a, epilogue, st);
     default: return mf_set_error("mf_gemm: bad tile id", -2);
   }

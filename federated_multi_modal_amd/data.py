@@ -74,9 +74,10 @@ class SyntheticClientDataManager:
                  unique_images: int = 0):
         """captions: batches carry one synthetic caption string per image (the caption-fork datasets' Datum
         captions), which turns on the caption-conditioned prompts; off, "caption" is None (BASELINE's
-        synthetic configs carry no captions).  unique_images > 0: each split generates that many images
-        (rounded up to the 64-image chunk) and repeats them to its size -- the device work per batch is the
-        same, and the host PRNG (~25 ms per image) stays out of long timing runs (bench.py's round wall-time)."""
+        synthetic configs carry no captions).  unique_images > 0: each split generates min(size, unique_images)
+        images (with their labels and, with captions, their captions) and repeats them in the same order to its
+        size -- the device work per batch is the same, and the host PRNG (~25 ms per image) stays out of long
+        timing runs (bench.py's round wall-time)."""
         self.client_id = client_id
         self._classnames = list(classnames)
         K = len(classnames)
@@ -91,10 +92,11 @@ class SyntheticClientDataManager:
                 imgs.append(torch.from_numpy(b.images).to(self.device))
                 labs.append(torch.from_numpy(b.labels).to(self.device))
             img, lab = torch.cat(imgs), torch.cat(labs)
-            if n_gen < n:
+            caps = syn.synthetic_captions(seed, client_id, zlib.crc32(tag.encode()), n_gen) if captions else None
+            if n_gen < n:  # repeat images, labels and captions alike, so image i keeps its own caption
                 reps = (n + n_gen - 1) // n_gen
                 img, lab = img.repeat(reps, 1, 1, 1)[:n].contiguous(), lab.repeat(reps)[:n].contiguous()
-            caps = syn.synthetic_captions(seed, client_id, zlib.crc32(tag.encode()), n) if captions else None
+                caps = (list(caps) * reps)[:n] if caps is not None else None
             return _Split(img, lab, caps)
 
         self.train = make("train", n_train)

@@ -212,6 +212,8 @@ class FakeClient:
         self.abort_round = abort_round                 # a ValueError (not caught by the reference) that round
         self.events = []
         self.model = self
+        # MaPLe.timing's counters (trainers.py): 3 "steps" per completed local epoch
+        self.timing = {"train_s": 0.0, "test_s": 0.0, "fedavg_launch_s": 0.0, "steps": 0, "epochs": 0}
 
     def state_dict(self):
         return {"flat16": self.engine.flat16, "flat32": self.engine.flat32}
@@ -231,6 +233,8 @@ class FakeClient:
             self.events.append(("abort", ep))
             raise ValueError("NaN/Inf values in input image")
         self.local_update(self.client_id, round_idx, ep, self.engine)
+        self.timing["steps"] += 3
+        self.timing["epochs"] += 1
         if before_test is not None:
             self.events.append(("fedavg_start", ep))
             before_test()
@@ -310,10 +314,15 @@ def test_round_loop_distributed(world, per_rank, fail, late):
         assert err is None, err
         # MaPLeFederated.round_times: one record per round, its phases inside the round's wall time
         assert [r["round"] for r in rounds] == [1, 2]
-        for r in rounds:
-            parts = sum(r[k] for k in ("local_train_s", "local_test_s", "fedavg_launch_s", "fedavg_exposed_s",
-                                       "global_state_s", "global_test_s", "other_s"))
-            assert abs(parts - r["wall_s"]) < 1e-6 and r["wall_s"] >= 0.0 and r["clients"] == per_rank
+        for ri, r in enumerate(rounds):
+            phases = ("local_train_s", "local_test_s", "fedavg_launch_s", "fedavg_exposed_s", "global_state_s",
+                      "global_test_s", "other_s")
+            # other_s is the remainder, so the sum holds by construction: every phase must also be >= 0 (no phase
+            # double-counted), and the step / epoch counts must be the rank's completed local epochs
+            assert all(r[k] >= 0.0 for k in phases), r
+            assert abs(sum(r[k] for k in phases) - r["wall_s"]) < 1e-6 and r["clients"] == per_rank
+            epochs = sum(2 - (1 if ri in fail.get(c, ()) else 0) for c in range(rank * per_rank, (rank + 1) * per_rank))
+            assert r["epochs"] == epochs and r["steps"] == 3 * epochs, (r, epochs)
         for j, (p16, p32) in enumerate(weights):
             c = rank * per_rank + j
             assert torch.equal(p16, g16) and torch.equal(p32, g32), c
