@@ -236,6 +236,9 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (K=1000 text side) side metric")
     ap.add_argument("--no-caption-mode", action="store_true", help="skip the caption-batch (K19) side metric")
     ap.add_argument("--no-round", action="store_true", help="skip the FedAvg round wall-time (trainer) runs")
+    # engine options (EngineConfig; results bit-identical, for same-box A/B: scripts/bench_ab.sh)
+    ap.add_argument("--fused-qkv-attn", default="side", choices=["side", "none", "both", "vision", "text"])
+    ap.add_argument("--text-first", action="store_true", help="enqueue the text tower first after each fork")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -259,7 +262,8 @@ def main():
 
     t0 = time.time()
     names = syn.synthetic_classnames(K, seed)
-    eng = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed), device=dev)
+    eng = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed,
+                                   fused_qkv_attn=args.fused_qkv_attn, vision_first=not args.text_first), device=dev)
     eng.set_lr(0.0026)
     # two resident synthetic batches per client (client id = rank), alternated step to step
     batches = []
@@ -579,9 +583,7 @@ def main():
                 "traffic_source_algorithmic_bytes_per_launch": traffic_alg,
                 "traffic_over_algorithmic": traffic / traffic_alg if traffic and traffic_alg else None,
                 "kernel": "GEMM family: the hand-written gemm_nt_kernel / gemm8(s)_kernel launches (csrc/gemm.hip) -- "
-                          "every projection GEMM of both towers, fwd + bwd" + (
-                              "" if not ops.gemm_lib_wants(6368, 2304, 768, ops.EPI_BIAS) else
-                              " + the hipBLASLt-routed products (MAPFED_GEMM_LIB=1)"),
+                          "every projection GEMM of both towers, fwd + bwd",
                 "launches_per_step": ps["launches"] // 2,
                 "avg_launch_us": ps["avg_us"], "flop_per_launch": ps["flops_per_launch"]}
         by_tower = {}

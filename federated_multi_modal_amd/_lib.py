@@ -44,15 +44,9 @@ SIGNATURES = {
     "mf_small_linear_bwd_batch": [P, I, I, I, I, P],
     "mf_clip_head_fwd": [P, P, I, I, I, P, P, P, P, P, P, P],
     "mf_clip_loss_fwd_bwd": [P, P, P, P, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P],
-    "mf_gemm_resid_ln_supported": [I, I],
-    "mf_gemm_resid_ln": [P, L, P, L, P, P, L, P, L, P, P, P, L, P, P, I, I, I, P],
     "mf_layernorm_bwd_inject": [P, L, P, L, P, P, P, P, L, P, L, P, I, I, P, I, I, I, P],
     "mf_layernorm_fwd_inject": [P, L, P, P, P, L, P, P, I, I, P, I, I, I, P],
     "mf_gemm_splitk": [P, L, I, P, L, I, P, L, I, I, I, P, L, I, I, P],
-    "mf_gemm_lib_init": [P, L],
-    "mf_gemm_lib_enable": [I],
-    "mf_gemm_lib_wants": [I, I, I, I],
-    "mf_gemm_lib": [P, L, P, L, P, L, I, I, I, P, I, P],
     "mf_clip_loss_soft_fwd_bwd": [P, P, P, P, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P],
     "mf_argmax_correct": [P, I, I, P, P, P, P],
     "mf_optim_chunk_bytes": [],
@@ -73,8 +67,7 @@ SIGNATURES = {
 # functions that return a value, not a status
 _VALUE_FUNCS = {"mf_abi_version", "mf_layernorm_bwd_blocks", "mf_colsum_blocks", "mf_optim_chunk_bytes",
                 "mf_optim_chunk_elems", "mf_col_reduce_desc_bytes", "mf_small_linear_desc_bytes",
-                "mf_gemm_splitk_ws_floats", "mf_augment_ws_bytes", "mf_qkv_attention_supported",
-                "mf_gemm_lib_wants", "mf_gemm_resid_ln_supported"}
+                "mf_gemm_splitk_ws_floats", "mf_augment_ws_bytes", "mf_qkv_attention_supported"}
 # value functions whose return type is not int
 _RESTYPES = {"mf_augment_ws_bytes": ctypes.c_int64}
 

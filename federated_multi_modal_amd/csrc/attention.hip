@@ -18,8 +18,7 @@
 //   bwd:  L <= 224: one fused workgroup per head (dK, dV, then dQ from dS^T kept in LDS);
 //         longer: dK/dV kernel (Q and dO for the head in LDS) and dQ kernel (K and V in LDS), P
 //         recomputed from the saved LSE.
-// Forward kernels: attn_fwd4_kernel (L <= 256, scores in registers) and attn_fwd_kernel (two-pass;
-// 257..512 rows, and the MAPFED_ATTN_FWD=1 A/B baseline).
+// Forward kernel: attn_fwd4_kernel (scores in registers; 257..512 rows with one 8-wave workgroup per CU).
 // LDS images are [rows][64] fp16 with the 16-byte chunk XOR swizzle chunk ^ (row & 7).
 #include <algorithm>
 #include <cstdlib>
@@ -101,128 +100,6 @@ __device__ unsigned long long* g_astamps;
 #endif
 
 // ---------------------------------------------------------------------------------------------
-template <int LKP, bool CAUSAL>
-__global__ __launch_bounds__(512, 4) void attn_fwd_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
-                                                      f16* __restrict__ out, int64_t ld_out,
-                                                      float* __restrict__ lse, int ld_lse, int L, int H) {
-  constexpr int NKT = LKP / 16;
-  __shared__ __attribute__((aligned(16))) f16 sK[LKP * 64];
-  __shared__ __attribute__((aligned(16))) f16 sV[LKP * 64];
-  const int D = H * 64;
-  const int nh = blockIdx.x, n = nh / H, h = nh % H;
-  const f16* base = qkv + (int64_t)n * L * ld_qkv;
-  MF_ASTAMP(0);
-  stage_rows<LKP>(sK, base, ld_qkv, L, D + h * 64);
-  stage_rows<LKP>(sV, base, ld_qkv, L, 2 * D + h * 64);
-  stage_wait();
-  MF_ASTAMP(1);
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  // every wave takes 16-row tiles w, w + nw, ... of this head (the staged operands are shared)
-  for (int q0 = (blockIdx.y * nw + w) * 16; q0 < L; q0 += gridDim.y * nw * 16) {
-  const int fr = lane & 15, fg = lane >> 4;
-  const int q = q0 + fr;
-  const int qc = q < L ? q : L - 1;
-  f16x8 qf[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) qf[s] = *(const f16x8*)(base + (int64_t)qc * ld_qkv + h * 64 + 32 * s + 8 * fg);
-
-  // two passes over the keys, 32 at a time, so that no score array lives in registers:
-  //   1) raw S = K Q^T -> row max;  2) S again, P = exp((S - max) / 8) (fp32), l = sum P,
-  //   O += V^T fp16(P)  (the reference's single-block CPU flash kernel: P relative to the final row
-  //   max; the 1/8 scale and log2(e) are folded into one FMA before v_exp_f32).
-  // LDS offsets: 32*ks is a multiple of 8, so the chunk swizzle depends on the lane only and a key
-  // block just adds ks * 32 rows * 64 elements.
-  const int ii = lane & 15;
-  int koff[2][2], voff[4][2];
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const int row = 16 * hf + fr;
-      koff[s2][hf] = row * 64 + (((4 * s2 + fg) ^ (row & 7)) << 3);
-    }
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) voff[dt][hf] = sw_off(16 * hf + 4 * fg + (ii >> 2), 16 * dt + 4 * (ii & 3));
-  }
-  const int kt_end = CAUSAL ? min(NKT, (q0 + 16 + 15) / 16) : NKT;
-  const int ks_end = (kt_end + 1) / 2;
-  auto scores = [&](int ks, f32x4& a0, f32x4& a1) {
-    a0 = (f32x4){0.f, 0.f, 0.f, 0.f};
-    a1 = a0;
-    const f16* kb = sK + ks * 32 * 64;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      a0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[s2][0]), qf[s2], a0, 0, 0, 0);
-      a1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)(kb + koff[s2][1]), qf[s2], a1, 0, 0, 0);
-    }
-    if (CAUSAL || 32 * ks + 32 > L) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key0 = 32 * ks + 4 * fg + i, key1 = key0 + 16;
-        if (key0 >= L || (CAUSAL && key0 > q)) a0[i] = -INFINITY;
-        if (key1 >= L || (CAUSAL && key1 > q) || 2 * ks + 1 >= kt_end) a1[i] = -INFINITY;
-      }
-    }
-  };
-  float m = -INFINITY;
-#pragma unroll 1
-  for (int ks = 0; ks < ks_end; ++ks) {
-    f32x4 a0, a1;
-    scores(ks, a0, a1);
-    m = fmaxf(m, fmaxf(fmaxf(a0[0], a0[1]), fmaxf(a0[2], a0[3])));
-    m = fmaxf(m, fmaxf(fmaxf(a1[0], a1[1]), fmaxf(a1[2], a1[3])));
-  }
-  MF_ASTAMP(2);
-  m = fmaxf(m, __shfl_xor(m, 16, 64));
-  m = fmaxf(m, __shfl_xor(m, 32, 64));
-  constexpr float kLog2eScale = 0.125f * 1.4426950408889634f;
-  const float mb = -m * kLog2eScale;
-  float l = 0.f;
-  f32x4 oacc[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) oacc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-  for (int ks = 0; ks < ks_end; ++ks) {
-    f32x4 a0, a1;
-    scores(ks, a0, a1);
-    f16x8 pf;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(a0[i], kLog2eScale, mb));
-      const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(a1[i], kLog2eScale, mb));
-      l += p0 + p1;
-      pf[i] = (f16)p0;
-      pf[4 + i] = (f16)p1;
-    }
-    const f16* vb = sV + ks * 32 * 64;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[dt][0]));
-      s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(vb + voff[dt][1]));
-      f16x8 vf = cat8(__builtin_bit_cast(f16x4, v0), __builtin_bit_cast(f16x4, v1));
-      oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf, oacc[dt], 0, 0, 0);
-    }
-  }
-  MF_ASTAMP(3);
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  m *= kScale;  // the scaled row max (for the LSE the backward recomputes P from)
-  if (q < L) {
-    const float inv = 1.0f / l;
-    f16* orow = out + ((int64_t)n * L + q) * ld_out + h * 64;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      f16x4 o;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] = (f16)(oacc[dt][i] * inv);
-      *(f16x4*)(orow + 16 * dt + 4 * fg) = o;
-    }
-    if (fg == 0) lse[(int64_t)nh * ld_lse + q] = m + __logf(l);
-  }
-  }
-}
-
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a constant)
 MF_DEV void wait_vmcnt(int n) {
   switch (n) {
@@ -339,12 +216,10 @@ MF_DEV void fwd4_tile(const f16* sK, const f16* sV, const int* koff, const int* 
   }
 }
 
-// Forward, single pass with register-resident scores: the grid / wave layout of attn_fwd_kernel
-// (16 queries per wave), but every score of the wave's queries (LKP keys x 16 queries = LKP/4 fp32 per
-// lane) is computed ONCE by independent back-to-back MFMAs and kept in registers; row max, exp, row
-// sum and the fp16 P pack then run from registers, and P . V follows.  Bit-identical to
-// attn_fwd_kernel (the same products in the same order; max is exact; the row sum and the P.V
-// accumulation keep its order) with a third fewer MFMAs and K reads and no per-chunk latency chain.
+// Forward, single pass with register-resident scores (16 queries per wave): every score of the wave's
+// queries (LKP keys x 16 queries = LKP/4 fp32 per lane) is computed ONCE by independent back-to-back MFMAs
+// and kept in registers; row max, exp, row sum and the fp16 P pack then run from registers, and P . V
+// follows (bit-identical to the two-pass form it replaced in r02, with a third fewer MFMAs and K reads).
 // Staging overlaps the first tile: its Q fragments are loaded first, then K, then V (LDS-DMA); the
 // scores start once Q and K have landed (vmcnt = this wave's V loads) and V is waited for only before
 // P.V, so the V transfer runs under the score MFMAs and the softmax.
@@ -1067,17 +942,11 @@ __global__ __launch_bounds__(64 * (LP / (16 * KT))) void attn_bwd_fused_kernel(
 
 inline int padded_len(int L) { return ((L + 31) / 32) * 32; }
 // one workgroup per (sequence, head): up to 8 waves sharing the staged operands, one 16-row tile each
-inline int attn_threads(int L) {
-  static const int maxw = getenv("MAPFED_ATTN_WAVES") ? atoi(getenv("MAPFED_ATTN_WAVES")) : 8;  // tuning knob
-  return 64 * std::max(1, std::min(maxw, (L + 15) / 16));
-}
+inline int attn_threads(int L) { return 64 * std::max(1, std::min(8, (L + 15) / 16)); }
 // query-tile split of a head over workgroups: enough workgroups to cover the chip (measured best:
 // 2 at N*H = 384, 4 at N*H = 48; tests/diagnostics/attn_bench.py), at the cost of re-staging K/V
 inline int attn_qsplit(int NH, int L) {
-  static const int qs = getenv("MAPFED_ATTN_QSPLIT") ? atoi(getenv("MAPFED_ATTN_QSPLIT")) : 0;  // tuning knob
-  // the text tower's short sequences (L <= 128) alone: MAPFED_ATTN_QSPLIT_TEXT (A/B knob)
-  static const int qst = getenv("MAPFED_ATTN_QSPLIT_TEXT") ? atoi(getenv("MAPFED_ATTN_QSPLIT_TEXT")) : 0;
-  const int want = (L <= 128 && qst > 0) ? qst : qs > 0 ? qs : std::min(4, (768 + NH - 1) / NH);
+  const int want = std::min(4, (768 + NH - 1) / NH);
   return std::max(1, std::min(want, (L + 15) / 16 / 2));
 }
 
@@ -1091,8 +960,7 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
   if (ld_lse < L || (ld_qkv % 8) || (ld_out % 4)) return mf_set_error("mf_attention_fwd: bad strides", -1);
   const int LP = padded_len(L);
   hipStream_t st = (hipStream_t)stream;
-  static const int fwd_variant = getenv("MAPFED_ATTN_FWD") ? atoi(getenv("MAPFED_ATTN_FWD")) : 4;  // A/B knob: 1 = attn_fwd_kernel
-  if (L > 256 && fwd_variant == 4) {
+  if (L > 256) {
     // register-resident scores at up to 512 keys: 8 waves (512 threads), 2 per SIMD, one workgroup per CU
     const int qs4 = attn_qsplit(N * H, L), tiles = (L + 15) / 16;
     const dim3 grid4(N * H, qs4), block4(64 * std::min(8, (tiles + qs4 - 1) / qs4));
@@ -1121,19 +989,10 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
     MF_CHECK_LAUNCH();
     return 0;
   }
-  if (L > 256) {
-    const dim3 grid(N * H, attn_qsplit(N * H, L)), block(attn_threads(L));
-#define CALLFL(P) attn_fwd_kernel<P, false><<<grid, block, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H);
-    MF_ATTN_DISPATCH_LONG(LP, CALLFL)
-#undef CALLFL
-    MF_CHECK_LAUNCH();
-    return 0;
-  }
-  if (fwd_variant == 4) {
+  {
     // the head's 16-query tiles split evenly over its workgroups (no workgroup without a tile)
     const int qs4 = attn_qsplit(N * H, L), tiles = (L + 15) / 16;
-    static const int fw = getenv("MAPFED_ATTN_FWD_WAVES") ? atoi(getenv("MAPFED_ATTN_FWD_WAVES")) : 0;  // A/B knob
-    const int nw4 = fw > 0 ? std::min(fw, (tiles + qs4 - 1) / qs4) : std::min(16, (tiles + qs4 - 1) / qs4);
+    const int nw4 = std::min(16, (tiles + qs4 - 1) / qs4);
     const dim3 grid4(N * H, qs4), block4(64 * nw4);
     const int LP16 = tiles * 16;  // keys staged in 16-row tiles (LP16 % 32 == 16: a half last chunk)
 #define CALLF4(P)                                                                                             \
@@ -1156,16 +1015,6 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
     MF_CHECK_LAUNCH();
     return 0;
   }
-  const dim3 grid(N * H, attn_qsplit(N * H, L)), block(attn_threads(L));
-#define CALLF(P)                                                                                            \
-  if (causal)                                                                                               \
-    attn_fwd_kernel<P, true><<<grid, block, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); \
-  else                                                                                                      \
-    attn_fwd_kernel<P, false><<<grid, block, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H);
-  MF_ATTN_DISPATCH(LP, CALLF)
-#undef CALLF
-  MF_CHECK_LAUNCH();
-  return 0;
 }
 
 extern "C" int mf_attention_bwd(const void* qkv, int64_t ld_qkv, const void* out, int64_t ld_out, const void* dout,
@@ -1193,24 +1042,15 @@ extern "C" int mf_attention_bwd(const void* qkv, int64_t ld_qkv, const void* out
     MF_CHECK_LAUNCH();
     return 0;
   }
-  // A/B knobs, read per call (host side only; a captured graph keeps the kernels it captured)
-  const int bwd_variant = getenv("MAPFED_ATTN_BWD") ? atoi(getenv("MAPFED_ATTN_BWD")) : 2;
-  if (bwd_variant == 2 && LP <= 224) {
-    static const int kt_w = getenv("MAPFED_ATTN_BWD_KT") ? atoi(getenv("MAPFED_ATTN_BWD_KT")) : 1;  // tuning knob
-    const dim3 gridf(N * H), blockf(64 * (LP / (16 * kt_w)));
+  if (LP <= 224) {  // one fused workgroup per (sequence, head), 16 keys per wave
+    const dim3 gridf(N * H), blockf(64 * (LP / 16));
 #define CALLBF(P)                                                                                                  \
   if (causal)                                                                                                      \
-    if (kt_w == 1) attn_bwd_fused_kernel<P, true, 1><<<gridf, blockf, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)out, ld_out, \
-                                                              (const f16*)dout, ld_dout, lse, ld_lse, (f16*)dqkv,   \
-                                                              ld_dqkv, L, H);                                      \
-    else attn_bwd_fused_kernel<P, true, 2><<<gridf, blockf, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)out, ld_out,     \
+    attn_bwd_fused_kernel<P, true, 1><<<gridf, blockf, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)out, ld_out,  \
                                                               (const f16*)dout, ld_dout, lse, ld_lse, (f16*)dqkv,   \
                                                               ld_dqkv, L, H);                                      \
   else                                                                                                             \
-    if (kt_w == 1) attn_bwd_fused_kernel<P, false, 1><<<gridf, blockf, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)out, ld_out, \
-                                                               (const f16*)dout, ld_dout, lse, ld_lse, (f16*)dqkv,  \
-                                                               ld_dqkv, L, H);                                     \
-    else attn_bwd_fused_kernel<P, false, 2><<<gridf, blockf, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)out, ld_out,    \
+    attn_bwd_fused_kernel<P, false, 1><<<gridf, blockf, 0, st>>>((const f16*)qkv, ld_qkv, (const f16*)out, ld_out, \
                                                                (const f16*)dout, ld_dout, lse, ld_lse, (f16*)dqkv,  \
                                                                ld_dqkv, L, H);
     switch (LP) {

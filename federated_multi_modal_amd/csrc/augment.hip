@@ -7,7 +7,7 @@
 //
 // Default: ONE launch per batch (aug_fused_kernel, one workgroup per (image, band of output rows),
 // taps and the band's uint8 intermediate rows in LDS).  When a batch's taps + band rows would not fit
-// 64 KB of LDS (downscale beyond ~6x), or with MAPFED_AUG_3PASS set, three launches instead, all
+// 64 KB of LDS (downscale beyond ~6x), three launches instead, all
 // byte work (HBM / L2 bound, no MFMA):
 //   1. coeff:      one thread per (image, axis, output index) computes Pillow's precompute_coeffs in
 //                  float64 with the same operation order (-ffp-contract=off) and the 22-bit
@@ -183,7 +183,7 @@ template <bool F16>
 __global__ __launch_bounds__(256) void aug_fused_kernel(const uint8_t* __restrict__ src, const AugBatchArg ba,
                                                         int b_base, int out_h, int out_w,
                                                         int bilinear, int band, int kh, int kv, int rows_max,
-                                                        int stage_w, float m0, float m1, float m2, float sd0,
+                                                        float m0, float m1, float m2, float sd0,
                                                         float sd1, float sd2, void* __restrict__ out) {
   extern __shared__ int aug_lds[];
   int* hk = aug_lds;                         // [out_w][kh]
@@ -205,22 +205,11 @@ __global__ __launch_bounds__(256) void aug_fused_kernel(const uint8_t* __restric
   if (nr > rows_max) nr = rows_max;  // unreachable: the host sizes rows_max from the band's span
   const int W = g[1];
   const uint8_t* img = src + ba.off[bl] + ((int64_t)(g[2] + y_first) * W + g[3]) * 3;
-  // stage_w > 0: the band's crop rows are first copied into LDS ([nr][stage_w] bytes, consecutive
-  // lanes on consecutive bytes), so the taps below read LDS instead of scattered global bytes
-  uint8_t* srow = tmp + rows_max * out_w * 3;
-  if (stage_w) {
-    const int cwb = g[5] * 3;
-    for (int i = threadIdx.x; i < nr * cwb; i += 256) {
-      const int r = i / cwb, c = i - r * cwb;
-      srow[r * stage_w + c] = img[(int64_t)r * W * 3 + c];
-    }
-    __syncthreads();
-  }
   for (int e = threadIdx.x; e < nr * out_w; e += 256) {
     const int r = e / out_w, x = e - r * out_w;
     const int2 bd = hb[x];
     const int* k = hk + x * kh;
-    const uint8_t* row = stage_w ? srow + r * stage_w + bd.x * 3 : img + ((int64_t)r * W + bd.x) * 3;
+    const uint8_t* row = img + ((int64_t)r * W + bd.x) * 3;
     int s0 = 1 << (PRECISION_BITS - 1), s1 = s0, s2 = s0;
     for (int t = 0; t < bd.y; ++t) {
       const int kt = k[t];
@@ -309,7 +298,7 @@ extern "C" int mf_augment(const void* src, int64_t src_bytes, const int64_t* src
   if (interp != 0 && interp != 1) return mf_set_error("mf_augment: interp is 0 (bicubic) or 1 (bilinear)", -1);
   if (!src || !src_off_host || !src_off || !geom_host || !out || !ws)
     return mf_set_error("mf_augment: null pointer", -1);
-  int max_rows = 1, kh = 1, kv = 1, max_cw = 1;
+  int max_rows = 1, kh = 1, kv = 1;
   double vscale = 1.0, vsupport = 0.0;  // the largest vertical scale / support over the batch
   const double fsup = interp == 1 ? 1.0 : 2.0;
   for (int b = 0; b < B; ++b) {
@@ -335,7 +324,6 @@ extern "C" int mf_augment(const void* src, int64_t src_bytes, const int64_t* src
       }
     }
     if (ch > max_rows) max_rows = ch;
-    if (cw > max_cw) max_cw = cw;
   }
   const AugDims d = aug_dims(B, out_h, out_w, max_rows);
   if (aug_ws_bytes(d) > ws_bytes) return mf_set_error("mf_augment: workspace too small", -1);
@@ -343,17 +331,13 @@ extern "C" int mf_augment(const void* src, int64_t src_bytes, const int64_t* src
   // fused path: the largest band (16 rows down to 1) whose taps + intermediate rows fit 64 KB of LDS;
   // a band of n output rows reads at most (n-1)*scale + 2*support + 2 intermediate rows.  Geometry and
   // offsets travel by value in the kernel arguments, 64 images per launch.
-  if (!getenv("MAPFED_AUG_3PASS")) {
+  {
     for (int band = 16; band >= 1; band /= 2) {
       int rows = (int)ceil((band - 1) * vscale + 2.0 * vsupport) + 3;
       if (rows > max_rows) rows = max_rows;
       const int kh2 = (kh + 1) & ~1, kv2 = (kv + 1) & ~1;  // even counts keep the int2 arrays aligned
       int64_t lds = aug_fused_lds(out_w, band, kh2, kv2, rows);
       if (lds > AUG_FUSED_LDS_MAX) continue;
-      const int sw = (max_cw * 3 + 15) / 16 * 16;  // staged source row bytes, when they fit too
-      // opt-in A/B (MAPFED_AUG_STAGE=1): measured slower at B = 32 on 256x256 images, 49 vs 36 us
-      const int stage_w = (!getenv("MAPFED_AUG_STAGE") || lds + (int64_t)rows * sw > AUG_FUSED_LDS_MAX) ? 0 : sw;
-      lds += (int64_t)rows * stage_w;
       for (int b0 = 0; b0 < B; b0 += AUG_ARG_IMAGES) {
         const int nb = B - b0 < AUG_ARG_IMAGES ? B - b0 : AUG_ARG_IMAGES;
         AugBatchArg ba;
@@ -363,10 +347,10 @@ extern "C" int mf_augment(const void* src, int64_t src_bytes, const int64_t* src
         const dim3 gf((out_h + band - 1) / band, nb);
         if (out_f16)
           aug_fused_kernel<true><<<gf, 256, lds, st>>>((const uint8_t*)src, ba, b0, out_h, out_w, interp, band, kh2,
-                                                       kv2, rows, stage_w, m0, m1, m2, s0, s1, s2, out);
+                                                       kv2, rows, m0, m1, m2, s0, s1, s2, out);
         else
           aug_fused_kernel<false><<<gf, 256, lds, st>>>((const uint8_t*)src, ba, b0, out_h, out_w, interp, band, kh2,
-                                                        kv2, rows, stage_w, m0, m1, m2, s0, s1, s2, out);
+                                                        kv2, rows, m0, m1, m2, s0, s1, s2, out);
         MF_CHECK_LAUNCH();
       }
       return 0;

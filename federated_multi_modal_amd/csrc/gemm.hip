@@ -1241,8 +1241,8 @@ __global__ __launch_bounds__(512) void gemm8sp_kernel(GemmArgs g) {
 int launch_tile8sp(const GemmArgs& a, int epi, hipStream_t st) {
   static const int ncu = [] {
     int d = 0, n = 0;
-    hipGetDevice(&d);
-    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
+    (void)hipGetDevice(&d);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
     return n > 0 ? n : 256;
   }();
   const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
@@ -1349,13 +1349,6 @@ int launch_kmajor(const GemmArgs& a, bool ta, bool tb, int epi, int tile, hipStr
 #undef MF_KM
 }
 
-// tile-rule A/B knob (MAPFED_GEMM_RULE=1: every vision product on 160x128, text on 128-row tiles;
-// 2: the text N = 512 products back on 64x64; 3: the vision QKV on the unstaggered 256x256 kernel)
-inline int gemm_rule() {
-  static const int r = getenv("MAPFED_GEMM_RULE") ? atoi(getenv("MAPFED_GEMM_RULE")) : 0;
-  return r;
-}
-
 // Tile -1 = "off the critical path": the products of the tower that runs beside the one setting the step
 // (the engine passes it: the text tower at c4, the vision tower at C5).  That tower's own latency has slack
 // (c4: text alone 2.46 ms against the vision tower's 4.80 ms, tests/diagnostics/tower_bound_probe.py), but its
@@ -1363,18 +1356,12 @@ inline int gemm_rule() {
 // products want the tile that does the most work per CU-second, not the lowest latency: 160x128 for every
 // row-major product of >= 2 048 rows (c4 text: 76..304 workgroups instead of the latency picks' 96x64 / 96x128
 // and hipBLASLt's 64x96, 248..744 workgroups): c4 step +2.9 % (same-box A/B, two rounds: 5 585 / 5 617 ->
-// 5 770 / 5 758 img/s; profiles/r03_v7_text_tile_ab.txt); C5 vision +0.6..0.8 %.  MAPFED_TEXT_TILE=<id> forces
-// another tile for them, -1 the latency picks (A/B knob).
-inline int text_tile() {
-  static const int t = getenv("MAPFED_TEXT_TILE") ? atoi(getenv("MAPFED_TEXT_TILE")) : 10;
-  return t;
-}
+// 5 770 / 5 758 img/s; profiles/r03_v7_text_tile_ab.txt); C5 vision +0.6..0.8 %.
+constexpr int kSideTile = 10;
 
 // XCD blocking (tile_of): the N-range count 2^xb minimising one XCD's operand footprint A/(8/2^xb) +
-// B/2^xb (bytes of the A rows and B rows it reads); MAPFED_GEMM_XB overrides (A/B knob, -1 = auto)
+// B/2^xb (bytes of the A rows and B rows it reads)
 inline int gemm_xcd_split(int M, int N, int K) {
-  static const int forced = getenv("MAPFED_GEMM_XB") ? atoi(getenv("MAPFED_GEMM_XB")) : -1;
-  if (forced >= 0) return std::min(forced, 3);
   const double a_bytes = 2.0 * M * K, b_bytes = 2.0 * N * K;
   int best = 0;
   double best_fp = 1e300;
@@ -1416,10 +1403,6 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int S, int M,
 
 }  // namespace
 
-extern "C" int mf_gemm_lib_wants(int M, int N, int K, int epilogue);
-extern "C" int mf_gemm_lib(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N,
-                           int K, const void* bias, int epilogue, void* stream);
-
 // C[M,N] = epilogue(op(A) . op(B)^T):  a_kmajor = 0: A[m][k] at A[m*lda + k], 1: A[k*lda + m];
 // b_kmajor = 0: B[n][k] at B[n*ldb + k], 1: B[k*ldb + n].
 extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb, int b_kmajor, void* C,
@@ -1449,28 +1432,26 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     if (tile <= 0) tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
     return launch_kmajor(a, a_kmajor != 0, b_kmajor != 0, epilogue, tile, st);
   }
-  // the plain / bias-only products the vendor library runs faster (blaslt.hip; off until mf_gemm_lib_init)
   // tile -1: a product of the tower off the step's critical path (throughput tiles, see text_tile)
-  const bool side = tile == -1 && M >= 2048 && text_tile() > 0;
-  if (tile == -1) tile = side ? text_tile() : 0;
-  if (tile == 0 && mf_gemm_lib_wants(M, N, K, epilogue))
-    return mf_gemm_lib(A, lda, B, ldb, C, ldc, M, N, K, bias, epilogue, stream);
+  const bool side = tile == -1 && M >= 2048;
+  if (tile == -1) tile = side ? kSideTile : 0;
   if (tile == 0) {  // heuristic: fill the 256 CUs (measured: tests/diagnostics/gemm_bench.py, gemm_stamps.cpp)
     const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
     if (t256 >= 192 && t256 <= 256 && K >= 512)
-      tile = gemm_rule() == 3 ? 22 : 20;  // one round of 256x256 tiles on one workgroup per CU (vision QKV: 225 tiles), gemm8s
+      tile = 40;  // one round of 256x256 tiles on one workgroup per CU (vision QKV: 225 tiles), gemm8s
     else if (M >= 16384 && K >= 512)  // the C5 text tower (M = 77 000): many rounds of tiles whatever the
-      // shape, so the tile's own efficiency decides (gemm_bench.py ... c5): 256x256 for N >= 1536 (r04: the
-      // in-projection N = 1536 746 against 678 TFLOP/s on 160x128, profiles/r04_v3_c5_gemm_tiles.txt), 160x128
-      // otherwise (+6..40 % over the M = 6368 picks on the N = 512 products)
-      tile = N >= 1536 ? 20 : 10;
+      // shape, so the tile's own efficiency decides (gemm_bench.py ... c5): the full-line 256x256 kernel for
+      // N >= 1536 or K >= 1024 (r05, profiles/r05_v1_gemm8f_c5.txt: c5.dh 878 -> 946, c5.dqkv 832 -> 905, c5.proj
+      // 827 -> 875, c5.fc 591 -> 612 TFLOP/s), 160x128 for the N = 512, K = 512 products (c5.out 623 / 581, c5.do
+      // 735 / 663 on 160x128 / 256x256)
+      tile = (N >= 1536 || K >= 1024) ? 40 : 10;
     else if (M >= 4096 && K >= 512)  // vision products (M = 6368), tests/diagnostics/gemm_bench.py:
       // N = 3072: 160x128 (960 tiles); N = 768: 96x128 (402 tiles, two workgroups per CU) for K >= 2048,
       // 160x64 (480 tiles) for K = 768; +6..37 % over the 128-row tiles
-      tile = (N > 1024 || gemm_rule() == 1) ? 10 : (K >= 2048 ? 15 : 16);
-    else if (M >= 2048 && N >= 1024 && K <= 768 && gemm_rule() != 1)
+      tile = N > 1024 ? 10 : (K >= 2048 ? 15 : 16);
+    else if (M >= 2048 && N >= 1024 && K <= 768)
       tile = N >= 2048 ? 15 : 26;  // text (M = 2926): c_fc and its dX on 96x128, QKV on 96x64
-    else if (M >= 2048 && N <= 768 && K >= 512 && gemm_rule() != 1 && gemm_rule() != 2)
+    else if (M >= 2048 && N <= 768 && K >= 512)
       tile = 26;  // text N = 512 products (out-proj, c_proj, their dX, dQKV): 96x64, 248 tiles, +5..20 % over 64x64
     else if (M < 2048 && K >= 512) {
       // the small clients' products (C2 / C3: B = 4 images, 796 rows; K = 10 classes, 770 rows), r04 sweep
@@ -1503,6 +1484,10 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     case 20: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8s(a, epilogue, st);
     case 21: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 2, 4>(a, epilogue, st);
     case 22: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 256, 2, 4>(a, epilogue, st);
+    case 41: return launch_tile<224, 96, 2, 2, 2>(a, epilogue, st);
+    case 42: return launch_tile<224, 96, 2, 2, 3>(a, epilogue, st);
+    case 43: return launch_tile<224, 128, 2, 2, 3>(a, epilogue, st);
+    case 44: return launch_tile<208, 96, 1, 2, 3>(a, epilogue, st);
     case 40: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8f(a, epilogue, st);
     case 27: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8sp(a, epilogue, st);
     default: return mf_set_error("mf_gemm: bad tile id", -2);
@@ -1543,9 +1528,8 @@ extern "C" int mf_gemm_splitk(const void* A, int64_t lda, int a_kmajor, const vo
   // (split_tile_of) for >= 96 output tiles, else the r02 order (slice = dispatch id / tiles).  Same-box A/B
   // (tests/diagnostics/splitk_bench.py, profiles/r03_v1_splitk_order_ab.txt, two runs each): slice-major
   // v.dW_proj 52.1 -> 48.1 us, v.dW_qkv 40.2 -> 38.4, v.dW_fc 51.6 -> 50.1; but v.dW_out (36 tiles x 8)
-  // 25.2 -> 26.9 and t.dW_fc (64 tiles x 4) 22.2 -> 24.1.  MAPFED_SPLITK_ORDER=0 / 1 forces one order.
-  static const int order = getenv("MAPFED_SPLITK_ORDER") ? atoi(getenv("MAPFED_SPLITK_ORDER")) : -1;
-  const bool slice_major = order < 0 ? tiles >= 96 : order != 0;
+  // 25.2 -> 26.9 and t.dW_fc (64 tiles x 4) 22.2 -> 24.1.
+  const bool slice_major = tiles >= 96;
   GemmArgs a{(const f16*)A, (const f16*)B, ws, nullptr, nullptr, nullptr, lda, ldb, (int64_t)N, 0, M, N, K, 1, ks,
              slice_major ? ((N > M) ? 1 : 0) : 2};
   int rc;

@@ -404,27 +404,11 @@ __global__ __launch_bounds__(HWB * 32) void ln_bwd2_kernel(const f16* __restrict
   }
 }
 
-// A/B knob: MAPFED_LN=1 selects the wave-per-row kernels
-
-// rows per half-wave of the D = 512 (text) LayerNorm forward (MAPFED_LN_TEXT_RPH, A/B knob)
-inline int ln_text_rph() {
-  static const int r = getenv("MAPFED_LN_TEXT_RPH") ? atoi(getenv("MAPFED_LN_TEXT_RPH")) : 1;
-  return r == 2 || r == 4 ? r : 1;
-}
-
 // one row per half-wave (16 half-waves per row block) when the row blocks alone cannot fill the chip: below 256
 // blocks (the c4 text tower's 183, the small clients' ~50; tests/diagnostics/ln_bench.py, r04: 8.43 -> 7.58 us at
-// 2 926 x 512, 8.11 -> 7.43 at 796 x 768; at 6 368 x 768, 398 blocks, 14.3 -> 15.7, so not there).
-// MAPFED_LN_BWD_WIDE=0 / 1 forces the 8 / 16 half-wave form (A/B knob)
-inline bool ln_bwd_wide(int nblk) {
-  static const int w = getenv("MAPFED_LN_BWD_WIDE") ? atoi(getenv("MAPFED_LN_BWD_WIDE")) : -1;
-  return w < 0 ? nblk < 256 : w != 0;
-}
-
-inline int ln_variant() {
-  static const int v = getenv("MAPFED_LN") ? atoi(getenv("MAPFED_LN")) : 2;
-  return v;
-}
+// 2 926 x 512, 8.11 -> 7.43 at 796 x 768; at 6 368 x 768, 398 blocks, 14.3 -> 15.7, so not there).  Both forms
+// produce bit-identical partials (measured r04); tests/test_kernels_gpu.py::test_layernorm covers both regimes.
+inline bool ln_bwd_wide(int nblk) { return nblk < 256; }
 
 }  // namespace
 
@@ -434,16 +418,11 @@ extern "C" int mf_layernorm_fwd(const void* x, int64_t ldx, const int* row_index
   if (rows <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const bool v16 = ((uintptr_t)x % 16 == 0) && ((uintptr_t)y % 16 == 0) && (ldx % 8 == 0) && (ldy % 8 == 0);
-  if (ln_variant() == 2 && v16 && (D == 768 || D == 512)) {
+  // 16-byte accesses, one row per half-wave (the wave-per-row kernels below take unaligned rows)
+  if (v16 && (D == 768 || D == 512)) {
     const dim3 g2((rows + 7) / 8);
-    const int rph = D == 512 ? ln_text_rph() : 1;
-    const dim3 gr((rows + 8 * rph - 1) / (8 * rph));
     if (D == 768)
       ln_fwd2_kernel<768><<<g2, 256, 0, st>>>((const f16*)x, ldx, row_index, gamma, beta, (f16*)y, ldy, mean, rstd, rows);
-    else if (rph == 2)
-      ln_fwd2_kernel<512, 2><<<gr, 256, 0, st>>>((const f16*)x, ldx, row_index, gamma, beta, (f16*)y, ldy, mean, rstd, rows);
-    else if (rph == 4)
-      ln_fwd2_kernel<512, 4><<<gr, 256, 0, st>>>((const f16*)x, ldx, row_index, gamma, beta, (f16*)y, ldy, mean, rstd, rows);
     else
       ln_fwd2_kernel<512><<<g2, 256, 0, st>>>((const f16*)x, ldx, row_index, gamma, beta, (f16*)y, ldy, mean, rstd, rows);
     MF_CHECK_LAUNCH();
@@ -475,7 +454,7 @@ extern "C" int mf_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int
   const bool v16 = ((uintptr_t)dy % 16 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)dx % 16 == 0) &&
                    (!dres || ((uintptr_t)dres % 16 == 0 && ldres % 8 == 0)) && lddy % 8 == 0 && ldx % 8 == 0 &&
                    lddx % 8 == 0;
-  if (ln_variant() == 2 && v16) {
+  if (v16) {
     if (D == 768 && ln_bwd_wide(nblk))
       ln_bwd2_kernel<768, 16><<<nblk, 512, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, row_index, gamma, mean,
                                                     rstd, (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows);
@@ -561,22 +540,14 @@ extern "C" int mf_layernorm_fwd_inject(void* x, int64_t ldx, const float* gamma,
   if (L <= 0 || rows % L || row0 < 0 || row0 + nrows > L) return mf_set_error("mf_layernorm_fwd_inject: rows", -1);
   hipStream_t st = (hipStream_t)stream;
   const bool v16 = ((uintptr_t)x % 16 == 0) && ((uintptr_t)y % 16 == 0) && (ldx % 8 == 0) && (ldy % 8 == 0);
-  if (ldx != D || !(ln_variant() == 2 && v16 && (D == 768 || D == 512))) {
+  if (ldx != D || !(v16 && (D == 768 || D == 512))) {
     const int rc = mf_prompt_inject_fwd(x, prompt, rows / L, L, row0, nrows, D, stream);
     return rc ? rc : mf_layernorm_fwd(x, ldx, nullptr, gamma, beta, y, ldy, mean, rstd, rows, D, stream);
   }
   const dim3 g2((rows + 7) / 8);
-  const int rph = D == 512 ? ln_text_rph() : 1;
-  const dim3 gr((rows + 8 * rph - 1) / (8 * rph));
   if (D == 768)
     ln_fwd2_kernel<768><<<g2, 256, 0, st>>>((const f16*)x, ldx, nullptr, gamma, beta, (f16*)y, ldy, mean, rstd, rows,
                                             prompt, L, row0, nrows);
-  else if (rph == 2)
-    ln_fwd2_kernel<512, 2><<<gr, 256, 0, st>>>((const f16*)x, ldx, nullptr, gamma, beta, (f16*)y, ldy, mean, rstd,
-                                               rows, prompt, L, row0, nrows);
-  else if (rph == 4)
-    ln_fwd2_kernel<512, 4><<<gr, 256, 0, st>>>((const f16*)x, ldx, nullptr, gamma, beta, (f16*)y, ldy, mean, rstd,
-                                               rows, prompt, L, row0, nrows);
   else
     ln_fwd2_kernel<512><<<g2, 256, 0, st>>>((const f16*)x, ldx, nullptr, gamma, beta, (f16*)y, ldy, mean, rstd, rows,
                                             prompt, L, row0, nrows);
@@ -599,7 +570,7 @@ extern "C" int mf_layernorm_bwd_inject(const void* dy, int64_t lddy, const void*
   const bool v16 = ((uintptr_t)dy % 16 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)dx % 16 == 0) &&
                    (!dres || ((uintptr_t)dres % 16 == 0 && ldres % 8 == 0)) && lddy % 8 == 0 && ldx % 8 == 0 &&
                    lddx % 8 == 0 && (uintptr_t)inj_part % 16 == 0;
-  if (!v16 || ln_variant() != 2) return mf_set_error("mf_layernorm_bwd_inject: needs 16-byte aligned rows", -1);
+  if (!v16) return mf_set_error("mf_layernorm_bwd_inject: needs 16-byte aligned rows", -1);
   const int nblk = mf_layernorm_bwd_blocks(rows);
   float* dg_part = workspace;
   float* db_part = workspace + (int64_t)nblk * D;

@@ -35,11 +35,6 @@ from .tokenizer import get_tokenizer
 
 F16, F32 = torch.float16, torch.float32
 N_CTX = 2
-# towers whose in-projection + attention forward run as one launch (MAPFED_FUSED_QKV_ATTN overrides: "1" both, "0"
-# neither, "vision" / "text" one); the default "side" fuses the tower that runs beside the other one on its
-# throughput tiles (tile -1, >= 2 048 rows: the text tower at c4, the vision tower at C5), chosen by the same-box
-# A/Bs in DESIGN.md §4
-FUSED_QKV_ATTN_DEFAULT = "side"
 
 
 @dataclass
@@ -67,6 +62,14 @@ class EngineConfig:
     # CLIP's BPE merges file (bpe_simple_vocab_16e6.txt.gz) for the prompt / caption token ids
     # (tokenizer.py); "" -> the seeded synthetic word-id tokenizer
     bpe_path: str = ""
+    # towers whose in-projection + attention forward run as one launch (mf_qkv_attention_fwd, bit-identical to the
+    # unfused pair): "side" (default) fuses the tower that runs beside the other one on its throughput tiles (tile
+    # -1, >= 2 048 rows: the text tower at c4, the vision tower at C5; same-box A/Bs in DESIGN.md §4), "none",
+    # "both", "vision" or "text" one tower
+    fused_qkv_attn: str = "side"
+    # enqueue (and capture) order of the two towers after each fork: the vision tower (the step's critical path)
+    # first, so its launches are dispatched ahead of the text tower's (False: text first, the measured baseline)
+    vision_first: bool = True
 
 
 def prompt_prefix(cfg: EngineConfig) -> Tuple[str, Optional[np.ndarray]]:
@@ -293,13 +296,12 @@ class _Tower:
         self.dQKV = e(R, 3 * D)
         self.dF = e(R, 4 * D)
         self.attn_ws = e(N * H * max(self.Ls), dt=F32)
-        # the in-projection + attention forward as one launch (mf_qkv_attention_fwd) where its shapes allow;
-        # MAPFED_FUSED_QKV_ATTN=0 selects the unfused pair (A/B), "vision" / "text" fuses that tower only
-        sel = os.environ.get("MAPFED_FUSED_QKV_ATTN", FUSED_QKV_ATTN_DEFAULT)
-        self.fused_qkv_attn = sel == "1" or ("vision" if name == "image_encoder" else "text") in sel.split(",")
-        # the out-projection, residual add and ln_2 in one launch (full-row tiles, csrc/rowln.hip; D = 768):
-        # bit-identical but 2.8 % slower on the c4 step, so opt-in: MAPFED_FUSED_LN2=1
-        self.fused_ln2 = os.environ.get("MAPFED_FUSED_LN2", "0") == "1" and ops.gemm_resid_ln_supported(D, D)
+        # the in-projection + attention forward as one launch (mf_qkv_attention_fwd) where its shapes allow
+        # (EngineConfig.fused_qkv_attn; "side" is resolved by MapleEngine once both towers exist)
+        sel = eng.cfg.fused_qkv_attn
+        if sel not in ("side", "none", "both", "vision", "text"):
+            raise ValueError(f"EngineConfig.fused_qkv_attn: {sel!r}")
+        self.fused_qkv_attn = sel == "both" or sel == ("vision" if name == "image_encoder" else "text")
         # GEMM tile rule of this tower's projections: 0 = latency picks (the tower that sets the step), -1 =
         # work-per-CU-second picks (the tower beside it; MapleEngine.__init__ decides, csrc/gemm.hip text_tile)
         self.tile = 0
@@ -307,13 +309,11 @@ class _Tower:
         self.lnb = ops.LNGradBatch(dev)
         self.cs_ws = e(ops.colsum_ws_floats(R, 4 * D), dt=F32)
         # split-K weight gradients of the trainable block (few output tiles, K = R tokens): fp32 partial
-        # planes, summed in a fixed order (MAPFED_DW_SPLITK=0: the single-pass K-major GEMM)
-        # (only where the automatic split count exceeds 1: few 128x128 output tiles)
-        use = os.environ.get("MAPFED_DW_SPLITK", "1") != "0"
+        # planes, summed in a fixed order (only where the automatic split count exceeds 1: few 128x128 output tiles)
         shapes = ((3 * D, D), (D, D), (4 * D, D), (D, 4 * D))
         Rl = Rs[-1]
         ws = {s: ops.gemm_splitk_ws_floats(s[0], s[1], Rl) for s in shapes}
-        self.dw_split = {s for s in shapes if use and ws[s] > s[0] * s[1]}
+        self.dw_split = {s for s in shapes if ws[s] > s[0] * s[1]}
         self.dw_ws = e(max(ws[s] for s in self.dw_split), dt=F32) if self.dw_split else None
 
     # -- parameters of block i
@@ -350,15 +350,10 @@ class _Tower:
                             epilogue=ops.EPI_BIAS, tile=self.tile)
                 ops.attention_fwd(self.QKV[i], N, L, H, self.causal, out=self.O[i], lse=self.LSE[i])
             h2 = self.H2[:R]
-            if self.fused_ln2:  # out_proj + residual + ln_2 in one launch (rowln.hip, bit-identical)
-                ops.gemm_resid_ln(self.O[i], self.p(i, "attn.out_proj.weight"), self.p(i, "attn.out_proj.bias"), x,
-                                  self.X1[i], self.p(i, "ln_2.weight"), self.p(i, "ln_2.bias"), h2, self.mean2[i],
-                                  self.rstd2[i])
-            else:
-                ops.gemm_nt(self.O[i], self.p(i, "attn.out_proj.weight"), self.X1[i],
-                            bias=self.p(i, "attn.out_proj.bias"), aux_in=x, epilogue=ops.EPI_BIAS_RESID, tile=self.tile)
-                ops.layernorm_fwd(self.X1[i], self.p(i, "ln_2.weight"), self.p(i, "ln_2.bias"), h2, self.mean2[i],
-                                  self.rstd2[i])
+            ops.gemm_nt(self.O[i], self.p(i, "attn.out_proj.weight"), self.X1[i],
+                        bias=self.p(i, "attn.out_proj.bias"), aux_in=x, epilogue=ops.EPI_BIAS_RESID, tile=self.tile)
+            ops.layernorm_fwd(self.X1[i], self.p(i, "ln_2.weight"), self.p(i, "ln_2.bias"), h2, self.mean2[i],
+                              self.rstd2[i])
             g = self.G[:R]
             ops.gemm_nt(h2, self.p(i, "mlp.c_fc.weight"), g, bias=self.p(i, "mlp.c_fc.bias"), aux_out=self.Fp[i],
                         epilogue=ops.EPI_BIAS_GELU, tile=self.tile)
@@ -435,8 +430,6 @@ class MapleEngine:
         size, same model), as trainers/maple.py:660-681 evaluates the model being trained."""
         self.cfg = cfg
         self.device = torch.device(device)
-        if ops.gemm_lib_default():  # MAPFED_GEMM_LIB=1: the hipBLASLt yardstick route (csrc/blaslt.hip), A/B only
-            ops.gemm_lib_init(self.device)
         self.tokenizer = get_tokenizer(cfg.bpe_path)  # prompts and captions (CLIP BPE or the synthetic ids)
         d = cfg.dims
         self.B, self.K, self.J = cfg.batch, len(cfg.classnames), cfg.prompt_depth
@@ -483,23 +476,17 @@ class MapleEngine:
         self._build_io()
         # the tower with less projection work per step runs beside the other one (the text tower at c4, the
         # vision tower at C5): its GEMMs take the work-per-CU-second tiles (csrc/gemm.hip, tile -1)
-        if os.environ.get("MAPFED_SIDE_TILES", "1") != "0":
-            vis_work = self.vis.N * self.vis.L * self.vis.D ** 2
-            txt_work = self.txt.N * self.txt.L * self.txt.D ** 2
-            (self.txt if txt_work <= vis_work else self.vis).tile = -1
-        if os.environ.get("MAPFED_FUSED_QKV_ATTN", FUSED_QKV_ATTN_DEFAULT) == "side":
+        vis_work = self.vis.N * self.vis.L * self.vis.D ** 2
+        txt_work = self.txt.N * self.txt.L * self.txt.D ** 2
+        (self.txt if txt_work <= vis_work else self.vis).tile = -1
+        if cfg.fused_qkv_attn == "side":
             # the side tower's in-projection + attention as one launch (the text tower at c4, the vision tower at
             # C5; r04 same-box A/Bs)
             for t in (self.vis, self.txt):
                 t.fused_qkv_attn = t.tile == -1 and t.Rs[0] >= 2048
         self.side = torch.cuda.Stream(device=self.device)
         self.overlap_towers = True  # False: both towers on the current stream (isolated kernel timing)
-        # enqueue (and capture) order of the two towers after the fork: the vision tower (the step's critical
-        # path) first, so its launches are dispatched ahead of the text tower's (MAPFED_TOWER_ORDER=text: the
-        # text tower first, the A/B baseline)
-        self.vision_first = os.environ.get("MAPFED_TOWER_ORDER", "vision") != "text"
-        # the optimizer step as mf_optimizer_step (MAPFED_FUSED_OPTIM=0: the four-call form, A/B knob)
-        self.fused_optim = os.environ.get("MAPFED_FUSED_OPTIM", "1") != "0"
+        self.vision_first = cfg.vision_first  # tower enqueue order after each fork (EngineConfig)
         self.step_count = 0
         self.momentum_initialised = False
 
@@ -879,8 +866,7 @@ class MapleEngine:
         ops.nonfinite_flag(self.img_in, self.input_flag)
         if self.soft_labels:
             ops.nonfinite_flag(self.soft_label_in, self.input_flag)
-        if not self.fused_optim:  # (else mf_optimizer_step latches the input flag into hyper[4] at the step's end)
-            torch.maximum(self.hyper[4:5], self.input_flag.to(F32), out=self.hyper[4:5])
+        # (mf_optimizer_step latches the input flag into hyper[4] at the step's end)
         main = torch.cuda.current_stream(self.device)
         side = self.side if self.overlap_towers else main
         side.wait_stream(main)
@@ -930,16 +916,10 @@ class MapleEngine:
         loss") at that step before its backward (trainers/maple.py:375-376), so neither that step nor any
         later one of the epoch updates the weights; the SGD kernels skip while halt is set.  The trainer
         clears it at the start of an epoch and reports the failure (MaPLe.run_epoch)."""
-        if self.fused_optim:  # the same four steps in three launches (mf_optimizer_step, bit-identical)
-            ops.optimizer_step(self.flat16, self.gflat16, self.mom16, self.flat32, self.gflat32, self.mom32, self.chunks,
-                               self.nchunks, self.cfg.max_grad_norm, self.norm_part, self.clip_out, self.hyper,
-                               self.loss_out[3:4], self.input_flag)
-        else:
-            torch.maximum(self.hyper[4:5], self.loss_out[3:4], out=self.hyper[4:5])
-            ops.clip_grad_norm(self.gflat16, self.gflat32, self.chunks, self.nchunks, self.cfg.max_grad_norm,
-                               self.norm_part, self.clip_out)
-            ops.sgd_step(self.flat16, self.gflat16, self.mom16, self.clip_out, self.hyper)
-            ops.sgd_step(self.flat32, self.gflat32, self.mom32, self.clip_out, self.hyper)
+        # the halt latch, clip coefficient and both flat buffers' SGD in three launches (mf_optimizer_step)
+        ops.optimizer_step(self.flat16, self.gflat16, self.mom16, self.flat32, self.gflat32, self.mom32, self.chunks,
+                           self.nchunks, self.cfg.max_grad_norm, self.norm_part, self.clip_out, self.hyper,
+                           self.loss_out[3:4], self.input_flag)
         # the momentum buffers now exist (first_step -> 0) unless the update was skipped
         self.hyper[3:4].mul_(self.hyper[4:5])  # device ops, legal inside graph capture
 

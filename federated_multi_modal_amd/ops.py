@@ -120,35 +120,6 @@ def _rec(ev):
         ev.record()
 
 
-# hipBLASLt for the plain / bias-only products it runs faster (csrc/blaslt.hip): one workspace per process
-GEMM_LIB_WS_BYTES = 64 << 20
-_LIB_WS: Optional[torch.Tensor] = None
-
-
-def gemm_lib_default() -> bool:
-    """The hipBLASLt route is an A/B yardstick, off unless MAPFED_GEMM_LIB=1 (csrc/blaslt.hip)."""
-    return os.environ.get("MAPFED_GEMM_LIB", "0") not in ("", "0")
-
-
-def gemm_lib_init(device) -> None:
-    """Create the hipBLASLt handle and hand it a workspace that outlives every captured graph (idempotent);
-    with the route enabled (MAPFED_GEMM_LIB=1 or gemm_lib_enable(True)) mf_gemm's heuristic tile path sends the
-    products mf_gemm_lib_wants() names to hipBLASLt."""
-    global _LIB_WS
-    if _LIB_WS is None:
-        _LIB_WS = torch.empty(GEMM_LIB_WS_BYTES, dtype=torch.uint8, device=device)
-        call("mf_gemm_lib_init", _p(_LIB_WS), GEMM_LIB_WS_BYTES)
-
-
-def gemm_lib_enable(on: bool) -> None:
-    """Route (True) or keep (False) the library-eligible products off the hand-written kernels."""
-    call("mf_gemm_lib_enable", int(bool(on)))
-
-
-def gemm_lib_wants(M: int, N: int, K: int, epilogue: int) -> bool:
-    return bool(call("mf_gemm_lib_wants", M, N, K, epilogue))
-
-
 def gemm_nt(A, B, C=None, bias=None, aux_in=None, aux_out=None, epilogue=EPI_NONE, tile=0):
     """C[M,N] = epi(A[M,K] . B[N,K]^T)."""
     M, K = A.shape
@@ -233,24 +204,6 @@ def layernorm_fwd(x, gamma, beta, y=None, mean=None, rstd=None, row_index=None):
     return y, mean, rstd
 
 
-
-def gemm_resid_ln_supported(N: int, K: int) -> bool:
-    return bool(call("mf_gemm_resid_ln_supported", N, K))
-
-
-def gemm_resid_ln(A, W, bias, R, C, gamma, beta, Y, mean, rstd):
-    """C = fp16(R + fp16(A . W^T + bias)) and Y, mean, rstd = LayerNorm(C) in one launch (rowln.hip;
-    bit-identical to gemm_nt(EPI_BIAS_RESID) + layernorm_fwd).  Probed as a GEMM (its FLOPs; bytes: the
-    product's operands and residual, X1 written, and the LayerNorm's Y / statistics written)."""
-    M, K = A.shape
-    N = W.shape[0]
-    ev = None
-    if _PROBE is not None and _PROBE.wants("gemm"):
-        ev = _PROBE.around(2.0 * M * N * K, _gemm_bytes(M, N, K, C, R) + 2.0 * M * N + 8.0 * M, _gkey(), (M, N, K, "resid_ln"))
-    call("mf_gemm_resid_ln", _p(A), _ld(A), _p(W), _ld(W), _p(bias), _p(R), _ld(R), _p(C), _ld(C), _p(gamma),
-         _p(beta), _p(Y), _ld(Y), _p(mean), _p(rstd), M, N, K, _s())
-    _rec(ev)
-    return C, Y
 
 
 def layernorm_fwd_inject(x, gamma, beta, y, mean, rstd, prompt, L, row0, nrows):

@@ -40,15 +40,6 @@ int mf_abi_version(void);
 int mf_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
                const void* bias, const void* aux_in, void* aux_out, int64_t ld_aux, int epilogue, int tile,
                void* stream);
-/* The block's out-projection, residual add and ln_2 in one launch (full-row tiles, rowln.hip):
- * C = X1 = fp16(R + fp16(A . W^T + bias)), Y = LayerNorm(X1; gamma, beta, eps 1e-5) fp16, mean / rstd fp32
- * per row.  Bit-identical to mf_gemm_nt(EPI_BIAS_RESID) + mf_layernorm_fwd.  N = 768, K % 32 == 0
- * (mf_gemm_resid_ln_supported).  Replaces clip/model.py:303-305 (out_proj), 350 (x + attn) and 351's
- * ln_2 (153-159).                                                                                 */
-int mf_gemm_resid_ln_supported(int N, int K);
-int mf_gemm_resid_ln(const void* A, int64_t lda, const void* W, int64_t ldw, const void* bias, const void* R,
-                     int64_t ldr, void* C, int64_t ldc, const float* gamma, const float* beta, void* Y, int64_t ldy,
-                     float* mean, float* rstd, int M, int N, int K, void* stream);
 /* General layouts: C[M,N] = epilogue(op(A) . op(B)^T) with
  *   a_kmajor = 0: A[m][k] at A[m*lda + k]  |  1: A[k*lda + m]   (e.g. dY^T of a weight gradient)
  *   b_kmajor = 0: B[n][k] at B[n*ldb + k]  |  1: B[k*ldb + n]   (e.g. nn.Linear W [out][in] in dX = dY . W)
@@ -67,18 +58,6 @@ int mf_gemm_splitk(const void* A, int64_t lda, int a_kmajor, const void* B, int6
                    int64_t ldc, int M, int N, int K, float* ws, int64_t ws_floats, int splits, int out_f16,
                    void* stream);
 int mf_gemm_splitk_ws_floats(int M, int N, int K, int splits);
-/* hipBLASLt for the plain library products (csrc/blaslt.hip): C[M,N] = A[M,K] . B[N,K]^T (+ bias, rounded
- * once to fp16: nn.Linear's fp16(acc + bias)), epilogue 0 (none) or 1 (bias), row-major fp16 operands.
- * mf_gemm_lib_init registers a device workspace (kept alive by the caller) and creates the handle; once it
- * ran, mf_gemm / mf_gemm_nt at tile 0 send the products mf_gemm_lib_wants names (the vision in-projection,
- * the c_fc dX products: faster in hipBLASLt on their shapes) to mf_gemm_lib.  mf_gemm_lib_enable(0) keeps
- * them on the hand-written kernels (A/B; also $MAPFED_GEMM_LIB=0).  Replaces: the same nn.Linear / autograd
- * products as mf_gemm_nt (clip/model.py:303-305 in-projection, :274-280 c_fc backward).              */
-int mf_gemm_lib_init(void* workspace, int64_t bytes);
-int mf_gemm_lib_enable(int on);
-int mf_gemm_lib_wants(int M, int N, int K, int epilogue);
-int mf_gemm_lib(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
-                const void* bias, int epilogue, void* stream);
 
 /* ---- LayerNorm (fp16 io, fp32 math; clip/model.py:153-159) --------------------------------
  * row_index (optional, int32): output row i normalises input row row_index[i]

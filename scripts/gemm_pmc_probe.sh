@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes (one counter group per run) over single GEMM launches (tests/diagnostics/gemm_one.py):
-# stall / LDS / MFMA counters of a tile on a shape.  CONFIGS="M,N,K,tile[,epi] ..."; LIB=1 routes tile 0 to the
-# hipBLASLt yardstick (MAPFED_GEMM_LIB=1) for the products it takes.
+# stall / LDS / MFMA counters of a tile on a shape.  CONFIGS="M,N,K,tile[,epi] ..."; tile -2 = torch.mm (the
+# hipBLASLt yardstick) on the same operands.
 set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -11,10 +11,10 @@ P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_LDS_DATA_FIFO_FULL SQ
 P3="SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM SQ_INSTS_VMEM SQ_INSTS_SALU SQ_INSTS_VALU"
 for c in ${CONFIGS:-8192,8192,8192,20}; do
   IFS=, read -r M N K T E <<< "$c"
-  tag=${c//,/_}${LIB:+_lib}
+  tag=${c//,/_}
   for p in 1 2 3; do
     ctr=P$p
-    ( [ -n "${LIB:-}" ] && export MAPFED_GEMM_LIB=1; timeout -s KILL 90 rocprofv3 --pmc ${!ctr} --kernel-trace -f csv -d gpurun_out/gpmc/${tag}_p$p -o run -- \
+    ( timeout -s KILL 90 rocprofv3 --pmc ${!ctr} --kernel-trace -f csv -d gpurun_out/gpmc/${tag}_p$p -o run -- \
       python3 tests/diagnostics/gemm_one.py $M $N $K $T 4 ${E:-0} > gpurun_out/gpmc/${tag}_p$p.log 2>&1 )
     rc=$?; echo "$c pass $p rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/gpmc/${tag}_p$p.log; exit $rc; }
   done

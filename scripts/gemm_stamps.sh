@@ -5,7 +5,7 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 (cd tests/diagnostics && hipcc -O3 -std=c++17 --offload-arch=gfx950 -DMF_GEMM_STAMPS \
-  -I../../federated_multi_modal_amd/csrc gemm_stamps.cpp -o ../../gpurun_out/gemm_stamps -L/opt/rocm/lib -lhipblaslt) > gpurun_out/gemm_stamps_build.log 2>&1
+  -I../../federated_multi_modal_amd/csrc gemm_stamps.cpp -o ../../gpurun_out/gemm_stamps) > gpurun_out/gemm_stamps_build.log 2>&1
 rc=$?; [ $rc -eq 0 ] || { echo "stamps build rc=$rc"; tail -5 gpurun_out/gemm_stamps_build.log; exit $rc; }
 IFS=';' read -ra SH <<< "${SHAPES:-77000 2048 512 3 20;77000 2048 512 4 20;6368 2304 768 1 20}"
 for s in "${SH[@]}"; do

@@ -14,13 +14,13 @@
 #   pmc_gemm   FETCH_SIZE / WRITE_SIZE passes over tests/diagnostics/gemm_traffic.py -> gpurun_out/gemm_traffic.json
 #   gemm       tests/diagnostics/gemm_bench.py $GEMM_TILES $GEMM_SET   (tile A/B per shape against hipBLASLt)
 #   digest     tests/diagnostics/step_digest.py $DIGEST_CFGS (bit-identity A/B of two trees: compare the lines)
-#   ab         interleaved bench A/B of env knobs: VARIANTS="A=1 B=2,C=3 -" ROUNDS times (scripts/bench_ab.sh)
+#   ab         interleaved bench A/B of bench.py options: VARIANTS="--text-first -" ROUNDS times (scripts/bench_ab.sh)
 #   attn       tests/diagnostics/attn_bench.py $ATTN_ARGS
 #   pmc_bench  FETCH / WRITE / MFMA-busy passes over a short bench run (scripts/gpu_pmc.sh -> gpurun_out/pmc_summary.json)
 #   pmc_attn   PMC passes over the attention kernels (scripts/attn_pmc.sh -> gpurun_out/attn_pmc_summary.json)
 #   pmc_probe  stall / LDS / MFMA counter passes over single GEMM launches (scripts/gemm_pmc_probe.sh; CONFIGS, LIB)
 #   stamps_gemm / stamps_attn / stamps_qkv   in-kernel timelines (scripts/{gemm,attn,qkv}_stamps.sh; SHAPES)
-#   ab_c5      interleaved C5 A/B of env knobs (scripts/ab_c5.sh; VARIANTS, ROUNDS)
+#   ab_c5      interleaved C5 A/B of bench.py options (scripts/ab_c5.sh; VARIANTS, ROUNDS)
 # Two-tree A/B (scripts/make_ab.sh REV, then scripts/ab_dirs.sh / ab_digest.sh) and ab_gemm_dirs.sh stay separate:
 # they need a second build of the library prepared on the CPU side first.
 set -u

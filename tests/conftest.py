@@ -20,14 +20,3 @@ def dev():
     if not torch.cuda.is_available():
         pytest.fail("GPU test selected but no GPU is visible")
     return torch.device("cuda:0")
-
-
-@pytest.fixture
-def handwritten_gemm(dev):
-    """Keep every product on the hand-written GEMM kernels for the test (the hipBLASLt yardstick route of
-    csrc/blaslt.hip off even under MAPFED_GEMM_LIB=1), for tests that compare two hand-written paths bit for bit."""
-    from federated_multi_modal_amd import ops
-    ops.gemm_lib_init(dev)
-    ops.gemm_lib_enable(False)
-    yield
-    ops.gemm_lib_enable(ops.gemm_lib_default())

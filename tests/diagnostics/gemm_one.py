@@ -1,7 +1,6 @@
 """Diagnostic (GPU box): a few launches of one GEMM tile on one shape, for rocprofv3 --pmc passes:
     python gemm_one.py M N K tile [reps] [epi]
-tile 0 with MAPFED_GEMM_LIB=1 and a product the yardstick route takes (e.g. 6368 2304 768 0 4 1: the vision
-in-projection with its bias) runs hipBLASLt's kernel instead, for a counter-by-counter comparison."""
+tile -2 runs torch.mm (hipBLASLt) on the same operands instead, for a counter-by-counter comparison."""
 import sys
 from pathlib import Path
 
@@ -19,9 +18,10 @@ A = torch.randn(M, K, device=dev).half()
 B = (torch.randn(N, K, device=dev) * K ** -0.5).half()
 C = torch.empty(M, N, device=dev, dtype=torch.float16)
 bias = (torch.randn(N, device=dev) * 0.1).half() if epi == ops.EPI_BIAS else None
-if ops.gemm_lib_default():
-    ops.gemm_lib_init(dev)
 for _ in range(reps):
-    ops.gemm_nt(A, B, C=C, bias=bias, epilogue=epi, tile=tile)
+    if tile == -2:
+        torch.mm(A, B.t(), out=C)
+    else:
+        ops.gemm_nt(A, B, C=C, bias=bias, epilogue=epi, tile=tile)
 torch.cuda.synchronize()
 print("ok", M, N, K, tile)

@@ -1,6 +1,6 @@
 """Diagnostic (GPU box): LayerNorm forward / backward kernel time (hipGraph-timed) and algorithmic
-GB/s on the c4 shapes (vision 6368 x 768, text 2926 x 512), with bit-pattern checksums so variants
-(MAPFED_LN, MAPFED_LN_RPH) that claim bit-identity can be compared across runs."""
+GB/s on the c4 shapes (vision 6368 x 768, text 2926 x 512), with bit-pattern checksums so variants (two
+builds of the library) that claim bit-identity can be compared across runs."""
 import sys
 from pathlib import Path
 

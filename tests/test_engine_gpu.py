@@ -236,17 +236,17 @@ def test_eot_truncated_text_tower_matches_full(dev):
     assert worst <= 1e-2
 
 
-def test_tower_order_does_not_change_results(dev, monkeypatch):
-    """The towers' enqueue order after each fork (MAPFED_TOWER_ORDER: vision first by default, text first as
-    the A/B baseline) only changes which stream's launches reach the GPU first: every reduction is
+def test_tower_order_does_not_change_results(dev):
+    """The towers' enqueue order after each fork (EngineConfig.vision_first: vision first by default, text first
+    as the A/B baseline) only changes which stream's launches reach the GPU first: every reduction is
     deterministic, so logits, loss and every gradient are bit-identical, eagerly and in a replayed graph."""
     J, K, B, seed = 3, 10, 4, 6
     names = syn.synthetic_classnames(K, seed)
     b = syn.client_batch(seed, 0, 0, B, K)
     out = []
     for order in ("vision", "text"):
-        monkeypatch.setenv("MAPFED_TOWER_ORDER", order)
-        e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed), device=dev)
+        e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed,
+                                     vision_first=order == "vision"), device=dev)
         assert e.vision_first == (order == "vision")
         e.set_lr(0.0026)
         e.load_batch(torch.from_numpy(b.images), torch.from_numpy(b.labels))
@@ -339,33 +339,35 @@ def test_c5_full_size_properties(dev):
     assert torch.equal(l0, l2) and s0 == s2
 
 
-def test_fused_qkv_attention_does_not_change_results(dev, monkeypatch, handwritten_gemm):
-    """The in-projection + attention forward as one launch against the unfused pair on the hand-written GEMM:
-    both towers fused (MAPFED_FUSED_QKV_ATTN=1), and the default ("side": the text tower, which runs beside the
-    vision tower at c4): logits, loss and every gradient bit-identical at the c4 client shape (J = 9, K = 38,
-    B = 32)."""
-    J, K, B, seed = 9, 38, 32, 2
+@pytest.mark.parametrize("K,variants", [(38, ("none", "both", "side")), (1000, ("none", "side"))], ids=["c4", "c5"])
+def test_fused_qkv_attention_does_not_change_results(dev, K, variants):
+    """The in-projection + attention forward as one launch against the unfused pair (EngineConfig.fused_qkv_attn):
+    at the c4 client shape (J = 9, K = 38, B = 32) both towers fused and the default ("side": the text tower, which
+    runs beside the vision tower), and at C5 (K = 1 000) the default, which fuses the VISION tower there (the side
+    tower: less projection work than the 77 000-row text tower) -- logits, loss and every gradient bit-identical
+    to the unfused step."""
+    J, B, seed = 9, 32, 2
     names = syn.synthetic_classnames(K, seed)
     b = syn.client_batch(seed, 0, 0, B, K)
     out = []
-    for fused in ("0", "1", None):
-        if fused is None:
-            monkeypatch.delenv("MAPFED_FUSED_QKV_ATTN", raising=False)
-        else:
-            monkeypatch.setenv("MAPFED_FUSED_QKV_ATTN", fused)
-        e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed), device=dev)
-        assert e.vis.fused_qkv_attn == (fused == "1") and e.txt.fused_qkv_attn == (fused != "0")
+    for fused in variants:
+        e = MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed, fused_qkv_attn=fused),
+                        device=dev)
+        side_vis = K > 100  # c4: the text tower is the side tower; C5: the vision tower
+        want_vis = fused == "both" or (fused == "side" and side_vis)
+        want_txt = fused == "both" or (fused == "side" and not side_vis)
+        assert e.vis.fused_qkv_attn == want_vis and e.txt.fused_qkv_attn == want_txt, fused
         e.load_batch(torch.from_numpy(b.images), torch.from_numpy(b.labels))
         logits = e.forward().clone()
         e.forward_backward()
         out.append((logits, e.loss(), {k: v.detach().clone() for k, v in e.grads().items()},
-                    e.vis.QKV[3].clone(), e.txt.O[5].clone()))
+                    e.vis.QKV[3].clone(), e.vis.O[3].clone(), e.txt.O[5].clone()))
         del e
         torch.cuda.empty_cache()
-    (lg0, l0, g0, q0, o0) = out[0]
-    for lg1, l1, g1, q1, o1 in out[1:]:
+    (lg0, l0, g0, q0, vo0, o0) = out[0]
+    for lg1, l1, g1, q1, vo1, o1 in out[1:]:
         assert torch.equal(lg0, lg1) and l0 == l1
-        assert torch.equal(q0, q1) and torch.equal(o0, o1)
+        assert torch.equal(q0, q1) and torch.equal(vo0, vo1) and torch.equal(o0, o1)
         for n in g0:
             assert torch.equal(g0[n], g1[n]), n
 

@@ -224,6 +224,18 @@ def test_fused_qkv_attention_shape_rule():
     assert b"fewer than" in h.mf_last_error()
 
 
+def test_product_library_has_one_gemm_path():
+    """The product library links no vendor GEMM and exports no route to one: every product of
+    the step runs on csrc/gemm.hip's kernels; torch.mm (hipBLASLt) stays a yardstick in tests/diagnostics only."""
+    import subprocess
+    from federated_multi_modal_amd import _lib
+    so = str(_lib.LIB_PATH)
+    dyn = subprocess.run(["readelf", "-d", so], capture_output=True, text=True, check=True).stdout
+    assert "NEEDED" in dyn and "hipblaslt" not in dyn.lower() and "rocblas" not in dyn.lower()
+    syms = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
+    assert "mf_gemm_lib" not in syms and "mf_gemm_nt" in syms
+
+
 def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
     from federated_multi_modal_amd import _lib
     monkeypatch.setattr(_lib, "_LIB", None)

@@ -121,18 +121,26 @@ def test_abi_validates_geometry_before_any_launch():
 @pytest.mark.gpu
 @pytest.mark.parametrize("path", ["fused", "3pass"])
 @pytest.mark.parametrize("interp", ["bicubic", "bilinear"])
-def test_device_train_transform_bit_exact(dev, interp, path, monkeypatch):
-    """Both device paths: the fused one-launch kernel (default) and the three-launch path."""
+def test_device_train_transform_bit_exact(dev, interp, path):
+    """Both device paths: the fused one-launch kernel, and the three-launch path mf_augment takes when a batch's
+    taps + band rows exceed the fused kernel's 64 KB of LDS (whole-image crops downscaled 12x bicubic / 20x
+    bilinear: 49 / 41 taps per output index, augment.hip)."""
     from federated_multi_modal_amd import transforms as D
     if path == "3pass":
-        monkeypatch.setenv("MAPFED_AUG_3PASS", "1")
-    imgs = _images(5, SHAPES)
+        side = 2688 if interp == "bicubic" else 4480
+        imgs = _images(5, [(side, side - 64), (side - 32, side)])
+    else:
+        imgs = _images(5, SHAPES)
     packed = D.pack_images(imgs, dev)
     tr = D.DeviceTransform(True, 224, interp, MEAN, STD, out_dtype=torch.float32,
                            generator=torch.Generator().manual_seed(7))
     geom = tr.geometry(packed.shapes)
+    if path == "3pass":  # whole-image crops resized straight to 224 x 224
+        for b, img in enumerate(imgs):
+            H, W = img.shape[:2]
+            geom[b] = np.array([H, W, 0, 0, H, W, 224, 224, 0, 0, b % 2], np.int32)
     geom[1, 10] = 1  # make sure both flip states are covered
-    geom[2, 10] = 0
+    geom[0 if path == "3pass" else 2, 10] = 0
     out32 = tr(packed, geom).cpu().numpy()
     tr16 = D.DeviceTransform(True, 224, interp, MEAN, STD, out_dtype=torch.float16)
     out16 = tr16(packed, geom).cpu()
@@ -221,13 +229,9 @@ def test_device_transform_extreme_downscale_falls_back_bit_exact(dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("stage", [True, False])
-def test_device_train_transform_small_images_staged_bit_exact(dev, stage, monkeypatch):
-    """PatternNet / EuroSAT-size images: the fused kernel reads the crop rows from global memory
-    (default), or with MAPFED_AUG_STAGE stages each band's crop rows in LDS first.  Both bit-exact."""
+def test_device_train_transform_small_images_bit_exact(dev):
+    """PatternNet / EuroSAT-size images (and ragged small ones) through the fused kernel: bit-exact."""
     from federated_multi_modal_amd import transforms as D
-    if stage:
-        monkeypatch.setenv("MAPFED_AUG_STAGE", "1")
     shapes = [(256, 256), (64, 64), (224, 224), (37, 51), (250, 200), (256, 256)]
     imgs = _images(12, shapes)
     packed = D.pack_images(imgs, dev)
