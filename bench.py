@@ -168,7 +168,12 @@ def side_config(name, dev, world, rank, steps=5, warmup=2, seed=0, eot_truncate=
     return out
 
 
-def fed_round_wall(name, world, rank, epochs=10, test_images=1000, shots=16, seed=1):
+# PatternNet's test split: 30 % of its 38 x 800 images (datasets/patternnet.py:33, 66-72 of the reference: 50 % train,
+# 20 % val, the rest test, unshuffled), which the reference's client evaluates after every local epoch
+PATTERNNET_TEST_IMAGES = 38 * 800 - int(0.5 * 38 * 800) - int(0.2 * 38 * 800)
+
+
+def fed_round_wall(name, world, rank, epochs=10, test_images=1000, shots=16, seed=1, eval_group=None):
     """The metric's second half, the FedAvg round wall-time (local epochs + tests +
     exchange), through the reference's trainer API: MaPLeFederated.train() (trainers/maple_fed.py:228-303)
     with one client per rank, FED.LOCAL_EPOCHS local epochs per round, each epoch a pass over the client's
@@ -192,7 +197,8 @@ def fed_round_wall(name, world, rank, epochs=10, test_images=1000, shots=16, see
                          "FED.NUM_CLIENTS", world, "FED.NUM_ROUNDS", 2, "FED.LOCAL_EPOCHS", epochs,
                          "MODEL.NUM_CLASSES", K, "DATASET.NUM_SHOTS", shots, "DATALOADER.TRAIN_X.BATCH_SIZE", B,
                          "FED.SYNTHETIC_TEST_IMAGES", test_images, "FED.SYNTHETIC_UNIQUE_IMAGES", 64,
-                         "TRAINER.MAPLE.PROMPT_DEPTH", J])
+                         "TRAINER.MAPLE.PROMPT_DEPTH", J]
+                        + (["TRAINER.MAPLE.EVAL_GROUP", eval_group] if eval_group is not None else []))
     cfg.freeze()
     with contextlib.redirect_stdout(io.StringIO()):  # the trainer's per-epoch prints (stdout carries the JSON line)
         tr = build_trainer(cfg)
@@ -207,7 +213,8 @@ def fed_round_wall(name, world, rank, epochs=10, test_images=1000, shots=16, see
     n_train = len(c0.dm.train_loader) * B
     out = {"workload": f"{name}: {desc}; {shots}-shot train split ({n_train} images, {len(c0.dm.train_loader)} "
                        f"steps per epoch), {test_images}-image test split in batches of "
-                       f"{cfg.DATALOADER.TEST.BATCH_SIZE}, {epochs} local epochs, {world} client(s), one per rank",
+                       f"{cfg.DATALOADER.TEST.BATCH_SIZE} ({cfg.TRAINER.MAPLE.EVAL_GROUP} per forward-only eval launch), "
+                       f"{epochs} local epochs, {world} client(s), one per rank",
            "round_wall_s": rec["wall_s"],
            "split_s": {k: rec[k] for k in keys if k != "wall_s"},
            "steps": rec["steps"], "train_ms_per_step": 1e3 * rec["local_train_s"] / max(rec["steps"], 1),
@@ -612,6 +619,11 @@ def main():
         for cname in dict.fromkeys(("c3", args.config)):
             log(f"[bench] FedAvg round wall-time ({cname}) ...")
             fed_round[cname] = fed_round_wall(cname, world, rank)
+        if args.config == "c4":  # the reference's own test cadence: PatternNet's whole test split after every epoch
+            for grp in (1, None):
+                key = "c4_patternnet_test_split" + ("_eval_group1" if grp == 1 else "")
+                log(f"[bench] FedAvg round wall-time ({key}: {PATTERNNET_TEST_IMAGES} test images per epoch) ...")
+                fed_round[key] = fed_round_wall("c4", world, rank, test_images=PATTERNNET_TEST_IMAGES, eval_group=grp)
 
     c5 = None
     if args.config == "c4" and not args.no_c5:

@@ -188,8 +188,12 @@ def extend_cfg(cfg: CfgNode) -> None:
     # only.  The causal mask makes every later position dead for the EOT features, so logits and loss are
     # bit-identical (tests/test_engine_gpu.py::test_eot_truncated_text_tower_matches_full); gradients agree
     # up to fp32 summation order (the GEMM tiles follow the smaller row count).
+    # EVAL_GROUP (MI355X addition): test() feeds this many TEST.BATCH_SIZE loader batches to one forward of a
+    # forward-only engine.  Every product accumulates each output in the same k order whatever the tile, and
+    # every other kernel is per row / per head, so a row's logits do not depend on the batch it is in
+    # (tests/test_trainers_gpu.py::test_eval_group_counts_bit_identical): larger launches, the same counts.
     cfg.TRAINER.MAPLE = CfgNode(dict(N_CTX=2, CTX_INIT="a photo of a", PREC="fp16", PROMPT_DEPTH=9,
-                                     EOT_TRUNCATE=False))
+                                     EOT_TRUNCATE=False, EVAL_GROUP=4))
     cfg.DATASET.SUBSAMPLE_CLASSES = "all"
     cfg.TRAINER.IVLP = CfgNode(dict(N_CTX_VISION=2, N_CTX_TEXT=2, CTX_INIT="a photo of a", PREC="fp16",
                                     PROMPT_DEPTH_VISION=9, PROMPT_DEPTH_TEXT=9))

@@ -27,7 +27,7 @@ enum Epi : int {
   EPI_NONE = 0,        // C = fp16(acc)
   EPI_BIAS = 1,        // C = fp16(acc + bias)
   EPI_BIAS_RESID = 2,  // C = fp16(R + fp16(acc + bias))        (R = aux_in, may alias C)
-  EPI_BIAS_GELU = 3,   // F = fp16(acc + bias) -> aux_out ; C = QuickGELU16(F)
+  EPI_BIAS_GELU = 3,   // F = fp16(acc + bias) -> aux_out (if not null: the backward's operand) ; C = QuickGELU16(F)
   EPI_DGELU = 4,       // dG = fp16(acc) ; C = QuickGELU16_bwd(dG, F = aux_in)
   EPI_F32 = 5,         // C(float) = acc
   EPI_RESID = 6,       // C = fp16(R + fp16(acc))               (no bias)
@@ -126,7 +126,7 @@ MF_DEV void epi8(const GemmArgs& g, int64_t m, int n, int cnt, const f16* t, f16
 #pragma unroll
       for (int e = 0; e < 8; ++e) out[e] = (f16)((float)aux[e] + (float)tv[e]);
     } else if constexpr (EPI == EPI_BIAS_GELU) {
-      st16_stream(g.aux_out + m * g.ld_aux + n, tv);
+      if (g.aux_out) st16_stream(g.aux_out + m * g.ld_aux + n, tv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float t2;
@@ -148,7 +148,7 @@ MF_DEV void epi8(const GemmArgs& g, int64_t m, int n, int cnt, const f16* t, f16
       o = (float)g.aux_in[m * g.ld_aux + n + e] + tvv;
     } else if constexpr (EPI == EPI_BIAS_GELU) {
       float t2;
-      g.aux_out[m * g.ld_aux + n + e] = (f16)tvv;
+      if (g.aux_out) g.aux_out[m * g.ld_aux + n + e] = (f16)tvv;
       o = quick_gelu16(tvv, &t2);
     } else if constexpr (EPI == EPI_DGELU) {
       o = quick_gelu16_bwd(tvv, (float)g.aux_in[m * g.ld_aux + n + e]);
@@ -985,6 +985,160 @@ __global__ __launch_bounds__(512) void gemm8f_kernel(GemmArgs g) {
   MF_STAMP(3);
 }
 
+// gemm8g<BM, BN>: gemm8f's staggered 8-wave main loop for tiles whose K-tile stage ((BM + BN) x 64 fp16) is at most
+// 40 KiB, so the ring holds S = 4 whole K-tiles: the tile counts that fill 256 CUs in whole rounds (160x128: 240
+// tiles of the N = 768 products at M = 6 368, 960 of the N = 3 072 ones) at one 8-wave workgroup per CU.  A K-tile
+// stage is one [BM + BN][64] full-line image (A rows, then B rows; 16-B chunk c of row r at c ^ (r & 7)) cut into
+// P = (BM + BN) / 8 pieces of 8 rows (one LDS-DMA wave instruction each); wave w issues pieces w, w + 8, .. of a
+// K-tile, its j-th one in phase j % 4.  K-tile u is issued during K-tile u - 2 and retired (vmcnt = the wave's
+// pieces of u + 1, then the barrier) in the memory section of phase 4u - 1.  Waves 2 (M) x 4 (N), each (BM / 2) x
+// (BN / 4); phases (m-part, k-sub) as gemm8s / gemm8f (m-part 0 = the first ceil(TM / 2) row blocks), so every
+// accumulator sums its k-subs in ascending order: bit-identical to the other tiles.  Hazards under the one-barrier
+// stagger (gemm8f's model): RAW as gemm8f; WAR: slot u mod 4 held K-tile u - 4, last read in phase 4u - 13,
+// refilled from phase 4u - 8 (>= last read + 2).
+template <int BM, int BN, int EPI>
+__global__ __launch_bounds__(512) void gemm8g_kernel(GemmArgs g) {
+  constexpr int WN = 4, NT = 512;
+  constexpr int WTM = BM / 2, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int TM0 = (TM + 1) / 2, TM1 = TM - TM0;
+  static_assert(WTM % 16 == 0 && WTN % 16 == 0 && TM >= 2, "wave tile");
+  constexpr int P = (BM + BN) / 8;  // pieces per K-tile
+  constexpr int PW_LO = P / 8, PW_HI = (P + 7) / 8, P_HI_WAVES = P % 8;
+  constexpr int STAGE = (BM + BN) * BK;
+  constexpr int S = 4;
+  constexpr int LDC = BN + 8;
+  constexpr int LDS_ELEMS = S * STAGE > BM * LDC ? S * STAGE : BM * LDC;
+  static_assert(LDS_ELEMS * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) f16 lds[LDS_ELEMS];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  int mt, nt;
+  tile_of(wgid, (g.M + BM - 1) / BM, tiles_n, g.xb, mt, nt);
+  const int m0 = mt * BM;
+  const int n0 = nt * BN;
+
+  const int lrow = lane >> 3, schunk = (lane & 7) ^ lrow;
+  const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.A, 0, (int)(((int64_t)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t b_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.B, 0, (int)(((int64_t)(g.N - 1) * g.ldb + g.K) * 2), 0x00020000);
+  const int a_voff = (lrow * (int)g.lda + schunk * 8) * 2;
+  const int b_voff = (lrow * (int)g.ldb + schunk * 8) * 2;
+  auto stage = [&](int u) { return lds + (u % S) * STAGE; };
+  // this wave's pieces of K-tile u that belong to phase f (piece p = wid + 8j, j % 4 == f)
+  auto issue = [&](int u, int f) {
+    f16* dst = stage(u);
+    const int kofs = u * BK;
+#pragma unroll
+    for (int j = f; j < PW_HI; j += 4) {
+      const int p = wid + 8 * j;
+      if (p < P) {
+        if (p < BM / 8)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(dst + p * 8 * BK), 16,
+                                                   a_voff + (int)(((int64_t)(m0 + 8 * p) * g.lda + kofs) * 2), 0, 0, 0);
+        else
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              b_rsrc, (lds_ptr_t)(dst + p * 8 * BK), 16,
+              b_voff + (int)(((int64_t)(n0 + 8 * (p - BM / 8)) * g.ldb + kofs) * 2), 0, 0, 0);
+      }
+    }
+  };
+  auto issue_all = [&](int u) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) issue(u, f);
+  };
+  // retire all but this wave's pieces of one K-tile
+  auto wait_one_tile = [&]() {
+    if (wid < P_HI_WAVES) wait_vmcnt<PW_HI>();
+    else wait_vmcnt<PW_LO>();
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fg = lane >> 4;
+  const int foff0 = fr * BK + ((fg ^ (fr & 7)) << 3);
+  const int foff1 = fr * BK + (((4 + fg) ^ (fr & 7)) << 3);
+  const int a_row = wm * WTM, b_row = BM + wn * WTN;
+  auto read_a = [&](f16x8 (&af)[TM0], const f16* img, int part, int foff) {
+#pragma unroll
+    for (int i = 0; i < (part ? TM1 : TM0); ++i)
+      af[i] = *(const f16x8*)(img + (a_row + (part * TM0 + i) * 16) * BK + foff);
+  };
+  auto read_b = [&](f16x8 (&bf)[TN], const f16* img, int foff) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bf[j] = *(const f16x8*)(img + (b_row + j * 16) * BK + foff);
+  };
+  auto mma = [&](const f16x8 (&af)[TM0], const f16x8 (&bf)[TN], int part) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < (part ? TM1 : TM0); ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[part * TM0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[part * TM0 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = g.K / BK;  // >= 2
+  issue_all(0);
+  issue_all(1);
+  wait_one_tile();  // K-tile 0 landed (K-tile 1 in flight)
+  lds_barrier();
+  if (wm == 1) lds_barrier();  // the stagger
+  f16x8 fx[TM0], fy[TM0], fb0[TN], fb1[TN];
+
+  // MODE 0: t < nk - 2 (issues K-tile t + 2, retires t + 1 with t + 2 in flight); 1: t = nk - 2 (retires
+  // t + 1 = the last with nothing in flight); 2: t = nk - 1
+  auto ktile = [&](int kt, auto mode_tag) {
+    constexpr int MODE = decltype(mode_tag)::value;
+    const f16* img = stage(kt);
+    read_a(fx, img, 0, foff0);
+    read_b(fb0, img, foff0);
+    if constexpr (MODE == 0) issue(kt + 2, 0);
+    lds_barrier();
+    mma(fx, fb0, 0);
+    lds_barrier();
+    read_a(fy, img, 1, foff0);
+    if constexpr (MODE == 0) issue(kt + 2, 1);
+    lds_barrier();
+    mma(fy, fb0, 1);
+    lds_barrier();
+    read_a(fx, img, 1, foff1);
+    read_b(fb1, img, foff1);
+    if constexpr (MODE == 0) issue(kt + 2, 2);
+    lds_barrier();
+    mma(fx, fb1, 1);
+    lds_barrier();
+    read_a(fy, img, 0, foff1);
+    if constexpr (MODE == 0) {
+      issue(kt + 2, 3);
+      wait_one_tile();
+    } else if constexpr (MODE == 1) {
+      wait_vmcnt<0>();
+    }
+    lds_barrier();
+    mma(fy, fb1, 0);
+    lds_barrier();
+  };
+  for (int kt = 0; kt < nk - 2; ++kt) ktile(kt, std::integral_constant<int, 0>{});
+  ktile(nk - 2, std::integral_constant<int, 1>{});
+  ktile(nk - 1, std::integral_constant<int, 2>{});
+  if (wm == 0) lds_barrier();
+  __syncthreads();
+  epilogue_store<BM, BN, NT, TM, TN, EPI>(g, lds, acc, m0, n0, wm * WTM, wn * WTN, tid, fr, fg);
+}
+
 // Register-direct epilogue of the persistent kernel: the arithmetic of epilogue_store + epi8 (first rounding
 // fp16(acc + bias) / fp16(acc), then residual / QuickGELU / QuickGELU' in fp32 and one more fp16 rounding),
 // without the LDS staging pass, so the operand ring stays free for the next tile's first K-steps.  A lane's
@@ -1053,7 +1207,7 @@ MF_DEV void epilogue_regs(const GemmArgs& g, const f32x4 (&acc)[TM][TN], int m0,
 #pragma unroll
           for (int e = 0; e < 8; ++e) out[e] = (f16)((float)auxv[i][p][e] + (float)tv[e]);
         } else if constexpr (EPI == EPI_BIAS_GELU) {
-          st16_stream(g.aux_out + m * g.ld_aux + n, tv);
+          if (g.aux_out) st16_stream(g.aux_out + m * g.ld_aux + n, tv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             float t2;
@@ -1278,6 +1432,24 @@ int launch_tile8s(const GemmArgs& a, int epi, hipStream_t st) {
   return 0;
 }
 
+template <int BM, int BN>
+int launch_tile8g(const GemmArgs& a, int epi, hipStream_t st) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles), block(512);
+  switch (epi) {
+    case EPI_NONE: gemm8g_kernel<BM, BN, EPI_NONE><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS: gemm8g_kernel<BM, BN, EPI_BIAS><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_RESID: gemm8g_kernel<BM, BN, EPI_BIAS_RESID><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_GELU: gemm8g_kernel<BM, BN, EPI_BIAS_GELU><<<grid, block, 0, st>>>(a); break;
+    case EPI_DGELU: gemm8g_kernel<BM, BN, EPI_DGELU><<<grid, block, 0, st>>>(a); break;
+    case EPI_F32: gemm8g_kernel<BM, BN, EPI_F32><<<grid, block, 0, st>>>(a); break;
+    case EPI_RESID: gemm8g_kernel<BM, BN, EPI_RESID><<<grid, block, 0, st>>>(a); break;
+    default: return mf_set_error("mf_gemm_nt: bad epilogue", -2);
+  }
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
 int launch_tile8f(const GemmArgs& a, int epi, hipStream_t st) {
   const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
   dim3 grid(tiles), block(512);
@@ -1421,7 +1593,6 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     return mf_set_error("mf_gemm: epilogue needs bias", -1);
   if ((epilogue == EPI_BIAS_RESID || epilogue == EPI_DGELU || epilogue == EPI_RESID) && !aux_in)
     return mf_set_error("mf_gemm: epilogue needs aux_in", -1);
-  if (epilogue == EPI_BIAS_GELU && !aux_out) return mf_set_error("mf_gemm: epilogue needs aux_out", -1);
   const int vec8 = (ldc % 8 == 0) && (ld_aux % 8 == 0) && ((uintptr_t)C % 16 == 0) &&
                    (!aux_in || (uintptr_t)aux_in % 16 == 0) && (!aux_out || (uintptr_t)aux_out % 16 == 0);
   GemmArgs a{(const f16*)A, (const f16*)B, C, (const f16*)bias, (const f16*)aux_in, (f16*)aux_out,
@@ -1488,6 +1659,10 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     case 42: return launch_tile<224, 96, 2, 2, 3>(a, epilogue, st);
     case 43: return launch_tile<224, 128, 2, 2, 3>(a, epilogue, st);
     case 44: return launch_tile<208, 96, 1, 2, 3>(a, epilogue, st);
+    case 45: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8g<160, 128>(a, epilogue, st);
+    case 46: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8g<192, 128>(a, epilogue, st);
+    case 47: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8g<128, 128>(a, epilogue, st);
+    case 48: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8g<96, 192>(a, epilogue, st);
     case 40: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8f(a, epilogue, st);
     case 27: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8sp(a, epilogue, st);
     default: return mf_set_error("mf_gemm: bad tile id", -2);

@@ -70,6 +70,10 @@ class EngineConfig:
     # enqueue (and capture) order of the two towers after each fork: the vision tower (the step's critical path)
     # first, so its launches are dispatched ahead of the text tower's (False: text first, the measured baseline)
     vision_first: bool = True
+    # forward-only engine (test(): trainers/maple.py:660-681): the towers keep one set of per-block buffers
+    # (the forward's intermediates are not saved for a backward) and allocate no gradient buffers, so the eval
+    # engine can run large batches; the kernels and their results are those of the training engine's forward
+    inference: bool = False
 
 
 def prompt_prefix(cfg: EngineConfig) -> Tuple[str, Optional[np.ndarray]]:
@@ -264,6 +268,12 @@ class _Tower:
         R = max(Rs)
         self.R = R
         e = lambda *s, dt=F16: torch.empty(*s, device=dev, dtype=dt)
+        self.inference = bool(eng.cfg.inference)
+        if self.inference:
+            if any(self.grow):
+                raise NotImplementedError("EngineConfig.inference with growing (caption) sequences")
+            self._alloc_forward_only(e, R, N, H, D, layers)
+            return
         # X[i]: input of block i (X[layers]: the tower's output); Y[i]: block i's output buffer -- X[i+1] itself
         # unless block i+1 grows the sequence
         self.X = [e(Rs[0], D)]
@@ -316,6 +326,25 @@ class _Tower:
         self.dw_split = {s for s in shapes if ws[s] > s[0] * s[1]}
         self.dw_ws = e(max(ws[s] for s in self.dw_split), dt=F32) if self.dw_split else None
 
+    def _alloc_forward_only(self, e, R, N, H, D, layers):
+        """Inference buffers: block i reads X[i] and writes X[i + 1], so two alternating activation buffers
+        serve every block; each per-block intermediate list aliases one buffer (nothing is kept for a
+        backward)."""
+        xb = (e(R, D), e(R, D))
+        self.X = [xb[i % 2] for i in range(layers + 1)]
+        self.Y = self.X[1:]
+        one = lambda *s, dt=F16: [e(*s, dt=dt)] * layers
+        self.QKV, self.O, self.X1, self.Fp = one(R, 3 * D), one(R, D), one(R, D), one(R, 4 * D)
+        self.LSE = one(N * H * self.L, dt=F32)
+        self.mean1, self.rstd1, self.mean2, self.rstd2 = (one(R, dt=F32) for _ in range(4))
+        self.H1, self.H2, self.G = e(R, D), e(R, D), e(R, 4 * D)
+        self.dX = self.dX2 = self.dX1 = self.dO = self.dH = self.dQKV = self.dF = self.attn_ws = None
+        self.fused_qkv_attn = self.e.cfg.fused_qkv_attn in ("both", "vision" if self.name == "image_encoder"
+                                                             else "text")
+        self.tile = 0
+        self.lnb = self.cs_ws = self.dw_ws = None
+        self.dw_split = set()
+
     # -- parameters of block i
     def p(self, i: int, key: str) -> torch.Tensor:
         return self.e.P[f"{self.name}.transformer.resblocks.{i}.{key}"]
@@ -355,8 +384,9 @@ class _Tower:
             ops.layernorm_fwd(self.X1[i], self.p(i, "ln_2.weight"), self.p(i, "ln_2.bias"), h2, self.mean2[i],
                               self.rstd2[i])
             g = self.G[:R]
-            ops.gemm_nt(h2, self.p(i, "mlp.c_fc.weight"), g, bias=self.p(i, "mlp.c_fc.bias"), aux_out=self.Fp[i],
-                        epilogue=ops.EPI_BIAS_GELU, tile=self.tile)
+            # the pre-activation is kept for the backward (QuickGELU'); a forward-only engine skips its store
+            ops.gemm_nt(h2, self.p(i, "mlp.c_fc.weight"), g, bias=self.p(i, "mlp.c_fc.bias"),
+                        aux_out=None if self.inference else self.Fp[i], epilogue=ops.EPI_BIAS_GELU, tile=self.tile)
             ops.gemm_nt(g, self.p(i, "mlp.c_proj.weight"), self.Y[i], bias=self.p(i, "mlp.c_proj.bias"),
                         aux_in=self.X1[i], epilogue=ops.EPI_BIAS_RESID, tile=self.tile)
             if i + 1 < self.layers and self.grow[i + 1]:
@@ -375,6 +405,8 @@ class _Tower:
         """self.dX[:Rs[-1]] holds d(loss)/d(X[layers]).  On return self.dX[:Rs[0]] = d(loss)/d(X[0]) (the
         injected rows of prompted layers reduced into prompt_grads[j] for the prompt injected before layer
         j+1)."""
+        if self.inference:
+            raise RuntimeError("backward on a forward-only (EngineConfig.inference) engine")
         N, D, H = self.N, self.D, self.H
         last = self.layers - 1
         for i in reversed(range(self.layers)):

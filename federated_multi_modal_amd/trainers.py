@@ -354,31 +354,53 @@ class MaPLe(TrainerX):
     # ---------------------------------------------------------------- evaluation
     def _evaluator(self, batch_size: int) -> MapleEngine:
         if self._eval_engine is None or self._eval_engine.B != batch_size:
-            ecfg = dataclasses.replace(self.engine.cfg, batch=batch_size)
+            self._eval_engine = None  # free the old buffers first
+            # forward-only: one set of per-block buffers, no gradients (EngineConfig.inference)
+            ecfg = dataclasses.replace(self.engine.cfg, batch=batch_size, inference=not self.engine.cfg.captions)
             self._eval_engine = MapleEngine(ecfg, device=self.device, shared=self.engine)
         return self._eval_engine
 
     def test(self, evaluate_train: bool = False):
-        """trainers/maple.py:660-681: accuracy (%) over the test loader; one host sync at the end."""
+        """trainers/maple.py:660-681: accuracy (%) over the test loader; one host sync at the end.
+
+        TRAINER.MAPLE.EVAL_GROUP loader batches go to one forward of the forward-only eval engine (a row's logits
+        do not depend on the batch it is in, so the counts are those of batch-by-batch evaluation)."""
         self.model.eval()
         loader = self.dm.test_loader
-        ev = self._evaluator(loader.batch)
+        group = max(1, int(self.cfg.TRAINER.MAPLE.get("EVAL_GROUP", 1)))
+        group = min(group, max(1, len(loader)))
+        ev = self._evaluator(loader.batch * group)
         self._acc.zero_()
-        # the class-prompt text features depend on the weights only: encoded by the first batch and
+        # the class-prompt text features depend on the weights only: encoded by the first launch and
         # reused by the rest of the pass (bit-identical; SURVEY.md §8(f) rank 1)
         reuse = False
-        for batch in loader:
-            x, y, _ = self.parse_batch_train(batch)
-            n = y.numel()
+        filled, labels = 0, []
+
+        def launch(n):
+            nonlocal reuse
+            y = labels[0] if len(labels) == 1 else torch.cat(labels)
             if n == ev.B:
-                ev.img_in.copy_(x)
                 ev.eval_batch(y, self._acc, reuse_text=reuse)
-            else:  # ragged last batch: pad the static buffer, count only the real rows
-                ev.img_in.zero_()
-                ev.img_in[:n].copy_(x)
+            else:  # ragged last launch: pad the static buffer, count only the real rows
+                ev.img_in[n:].zero_()
                 logits = ev.forward(reuse_text=reuse)
                 ops.argmax_correct(logits[:n], y, None, self._acc)
             reuse = True
+
+        for batch in loader:
+            x, y, _ = self.parse_batch_train(batch)
+            n = y.numel()
+            if filled + n > ev.B:  # (a loader batch never exceeds loader.batch; defensive)
+                launch(filled)
+                filled, labels = 0, []
+            ev.img_in[filled:filled + n].copy_(x)
+            labels.append(y)
+            filled += n
+            if filled == ev.B:
+                launch(filled)
+                filled, labels = 0, []
+        if filled:
+            launch(filled)
         correct, total = self._acc.tolist()
         acc = 100.0 * correct / total if total > 0 else 0.0
         print(f"[Client {self.client_id}] Test Accuracy: {acc:.2f}%")

@@ -397,3 +397,42 @@ def test_eot_truncate_config_key(dev, tmp_path):
         out.append((c.engine.logits.detach().cpu().clone(), c.engine.loss()))
     assert torch.equal(out[0][0], out[1][0])
     assert out[0][1] == out[1][1]
+
+
+def test_eval_group_counts_bit_identical(dev, tmp_path):
+    """test() with TRAINER.MAPLE.EVAL_GROUP loader batches per forward of the forward-only eval engine
+    (EngineConfig.inference): every row's logits equal those of the training engine's forward at the loader's
+    batch size, bit for bit (a ragged last batch included), so the accuracy counts of a test pass are those of
+    batch-by-batch evaluation (trainers/maple.py:660-681)."""
+    import dataclasses
+    from federated_multi_modal_amd.engine import MapleEngine
+    cfg = small_cfg(tmp_path, extra=["FED.SYNTHETIC_TEST_IMAGES", 30])
+    tr = build_trainer(cfg)
+    c = tr.clients[0]
+    for _ in range(2):  # weights away from the initial state
+        c.forward_backward(next(iter(c.dm.train_loader)))
+    X, Y = c.dm.test.images, c.dm.test.labels
+    n, b = Y.numel(), c.dm.test_loader.batch
+    assert n == 30 and b == 12
+    big = MapleEngine(dataclasses.replace(c.engine.cfg, batch=n, inference=True), device=dev, shared=c.engine)
+    big.img_in.copy_(X)
+    Lb = big.forward().clone()
+    small = MapleEngine(dataclasses.replace(c.engine.cfg, batch=b), device=dev, shared=c.engine)
+    rows = []
+    for s in range(0, n, b):
+        small.img_in.zero_()
+        small.img_in[:min(b, n - s)].copy_(X[s:s + b])
+        rows.append(small.forward().clone()[:min(b, n - s)])
+    Ls = torch.cat(rows)
+    assert torch.equal(Lb, Ls), (Lb.float() - Ls.float()).abs().max().item()
+    accs = []
+    for group in (1, 2, 4):
+        c.cfg.defrost()
+        c.cfg.TRAINER.MAPLE.EVAL_GROUP = group
+        c.cfg.freeze()
+        res = c.test()
+        accs.append((res["accuracy"], c._acc.tolist()))
+        assert c._eval_engine.B == b * min(group, 3) and c._eval_engine.cfg.inference
+    assert accs[0] == accs[1] == accs[2], accs
+    pred = Ls.float().argmax(1)
+    assert accs[0][1] == [float((pred == Y).sum().item()), float(n)]
