@@ -944,9 +944,12 @@ inline int padded_len(int L) { return ((L + 31) / 32) * 32; }
 // one workgroup per (sequence, head): up to 8 waves sharing the staged operands, one 16-row tile each
 inline int attn_threads(int L) { return 64 * std::max(1, std::min(8, (L + 15) / 16)); }
 // query-tile split of a head over workgroups: enough workgroups to cover the chip (measured best:
-// 2 at N*H = 384, 4 at N*H = 48; tests/diagnostics/attn_bench.py), at the cost of re-staging K/V
+// 2 at N*H = 384, 4 at N*H = 48; tests/diagnostics/attn_bench.py), at the cost of re-staging K/V.  Sequences
+// longer than 128 rows keep at least 2 whatever the head count (r05: the eval engine's 4 800 heads): a whole
+// 199-row head is a 13-wave workgroup, of which only one fits a CU (16 waves at 104 VGPRs), so its K/V staging
+// never overlaps another workgroup's tiles; two 7-wave halves do fit, two per CU.
 inline int attn_qsplit(int NH, int L) {
-  const int want = std::min(4, (768 + NH - 1) / NH);
+  const int want = std::max(L > 128 ? 2 : 1, std::min(4, (768 + NH - 1) / NH));
   return std::max(1, std::min(want, (L + 15) / 16 / 2));
 }
 

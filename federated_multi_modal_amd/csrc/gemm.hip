@@ -176,17 +176,9 @@ __device__ unsigned long long* g_stamps;
       }                                                                                            \
     }                                                                                              \
   } while (0)
-// per-tile stamps of the persistent kernel (index = tile position instead of blockIdx.x)
-#define MF_STAMPI(idx, slot)                                                                       \
-  do {                                                                                             \
-    if (threadIdx.x == 0) g_stamps[(size_t)(idx) * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
 #else
 #define MF_STAMP(slot) \
   do {                 \
-  } while (0)
-#define MF_STAMPI(idx, slot) \
-  do {                       \
   } while (0)
 #endif
 
@@ -985,436 +977,6 @@ __global__ __launch_bounds__(512) void gemm8f_kernel(GemmArgs g) {
   MF_STAMP(3);
 }
 
-// gemm8g<BM, BN>: gemm8f's staggered 8-wave main loop for tiles whose K-tile stage ((BM + BN) x 64 fp16) is at most
-// 40 KiB, so the ring holds S = 4 whole K-tiles: the tile counts that fill 256 CUs in whole rounds (160x128: 240
-// tiles of the N = 768 products at M = 6 368, 960 of the N = 3 072 ones) at one 8-wave workgroup per CU.  A K-tile
-// stage is one [BM + BN][64] full-line image (A rows, then B rows; 16-B chunk c of row r at c ^ (r & 7)) cut into
-// P = (BM + BN) / 8 pieces of 8 rows (one LDS-DMA wave instruction each); wave w issues pieces w, w + 8, .. of a
-// K-tile, its j-th one in phase j % 4.  K-tile u is issued during K-tile u - 2 and retired (vmcnt = the wave's
-// pieces of u + 1, then the barrier) in the memory section of phase 4u - 1.  Waves 2 (M) x 4 (N), each (BM / 2) x
-// (BN / 4); phases (m-part, k-sub) as gemm8s / gemm8f (m-part 0 = the first ceil(TM / 2) row blocks), so every
-// accumulator sums its k-subs in ascending order: bit-identical to the other tiles.  Hazards under the one-barrier
-// stagger (gemm8f's model): RAW as gemm8f; WAR: slot u mod 4 held K-tile u - 4, last read in phase 4u - 13,
-// refilled from phase 4u - 8 (>= last read + 2).
-template <int BM, int BN, int EPI>
-__global__ __launch_bounds__(512) void gemm8g_kernel(GemmArgs g) {
-  constexpr int WN = 4, NT = 512;
-  constexpr int WTM = BM / 2, WTN = BN / WN;
-  constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int TM0 = (TM + 1) / 2, TM1 = TM - TM0;
-  static_assert(WTM % 16 == 0 && WTN % 16 == 0 && TM >= 2, "wave tile");
-  constexpr int P = (BM + BN) / 8;  // pieces per K-tile
-  constexpr int PW_LO = P / 8, PW_HI = (P + 7) / 8, P_HI_WAVES = P % 8;
-  constexpr int STAGE = (BM + BN) * BK;
-  constexpr int S = 4;
-  constexpr int LDC = BN + 8;
-  constexpr int LDS_ELEMS = S * STAGE > BM * LDC ? S * STAGE : BM * LDC;
-  static_assert(LDS_ELEMS * 2 <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(1024))) f16 lds[LDS_ELEMS];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WN, wn = wid % WN;
-  const int tiles_n = (g.N + BN - 1) / BN;
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  int mt, nt;
-  tile_of(wgid, (g.M + BM - 1) / BM, tiles_n, g.xb, mt, nt);
-  const int m0 = mt * BM;
-  const int n0 = nt * BN;
-
-  const int lrow = lane >> 3, schunk = (lane & 7) ^ lrow;
-  const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.A, 0, (int)(((int64_t)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t b_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.B, 0, (int)(((int64_t)(g.N - 1) * g.ldb + g.K) * 2), 0x00020000);
-  const int a_voff = (lrow * (int)g.lda + schunk * 8) * 2;
-  const int b_voff = (lrow * (int)g.ldb + schunk * 8) * 2;
-  auto stage = [&](int u) { return lds + (u % S) * STAGE; };
-  // this wave's pieces of K-tile u that belong to phase f (piece p = wid + 8j, j % 4 == f)
-  auto issue = [&](int u, int f) {
-    f16* dst = stage(u);
-    const int kofs = u * BK;
-#pragma unroll
-    for (int j = f; j < PW_HI; j += 4) {
-      const int p = wid + 8 * j;
-      if (p < P) {
-        if (p < BM / 8)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(dst + p * 8 * BK), 16,
-                                                   a_voff + (int)(((int64_t)(m0 + 8 * p) * g.lda + kofs) * 2), 0, 0, 0);
-        else
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              b_rsrc, (lds_ptr_t)(dst + p * 8 * BK), 16,
-              b_voff + (int)(((int64_t)(n0 + 8 * (p - BM / 8)) * g.ldb + kofs) * 2), 0, 0, 0);
-      }
-    }
-  };
-  auto issue_all = [&](int u) {
-#pragma unroll
-    for (int f = 0; f < 4; ++f) issue(u, f);
-  };
-  // retire all but this wave's pieces of one K-tile
-  auto wait_one_tile = [&]() {
-    if (wid < P_HI_WAVES) wait_vmcnt<PW_HI>();
-    else wait_vmcnt<PW_LO>();
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int fr = lane & 15, fg = lane >> 4;
-  const int foff0 = fr * BK + ((fg ^ (fr & 7)) << 3);
-  const int foff1 = fr * BK + (((4 + fg) ^ (fr & 7)) << 3);
-  const int a_row = wm * WTM, b_row = BM + wn * WTN;
-  auto read_a = [&](f16x8 (&af)[TM0], const f16* img, int part, int foff) {
-#pragma unroll
-    for (int i = 0; i < (part ? TM1 : TM0); ++i)
-      af[i] = *(const f16x8*)(img + (a_row + (part * TM0 + i) * 16) * BK + foff);
-  };
-  auto read_b = [&](f16x8 (&bf)[TN], const f16* img, int foff) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) bf[j] = *(const f16x8*)(img + (b_row + j * 16) * BK + foff);
-  };
-  auto mma = [&](const f16x8 (&af)[TM0], const f16x8 (&bf)[TN], int part) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < (part ? TM1 : TM0); ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[part * TM0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[part * TM0 + i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  const int nk = g.K / BK;  // >= 2
-  issue_all(0);
-  issue_all(1);
-  wait_one_tile();  // K-tile 0 landed (K-tile 1 in flight)
-  lds_barrier();
-  if (wm == 1) lds_barrier();  // the stagger
-  f16x8 fx[TM0], fy[TM0], fb0[TN], fb1[TN];
-
-  // MODE 0: t < nk - 2 (issues K-tile t + 2, retires t + 1 with t + 2 in flight); 1: t = nk - 2 (retires
-  // t + 1 = the last with nothing in flight); 2: t = nk - 1
-  auto ktile = [&](int kt, auto mode_tag) {
-    constexpr int MODE = decltype(mode_tag)::value;
-    const f16* img = stage(kt);
-    read_a(fx, img, 0, foff0);
-    read_b(fb0, img, foff0);
-    if constexpr (MODE == 0) issue(kt + 2, 0);
-    lds_barrier();
-    mma(fx, fb0, 0);
-    lds_barrier();
-    read_a(fy, img, 1, foff0);
-    if constexpr (MODE == 0) issue(kt + 2, 1);
-    lds_barrier();
-    mma(fy, fb0, 1);
-    lds_barrier();
-    read_a(fx, img, 1, foff1);
-    read_b(fb1, img, foff1);
-    if constexpr (MODE == 0) issue(kt + 2, 2);
-    lds_barrier();
-    mma(fx, fb1, 1);
-    lds_barrier();
-    read_a(fy, img, 0, foff1);
-    if constexpr (MODE == 0) {
-      issue(kt + 2, 3);
-      wait_one_tile();
-    } else if constexpr (MODE == 1) {
-      wait_vmcnt<0>();
-    }
-    lds_barrier();
-    mma(fy, fb1, 0);
-    lds_barrier();
-  };
-  for (int kt = 0; kt < nk - 2; ++kt) ktile(kt, std::integral_constant<int, 0>{});
-  ktile(nk - 2, std::integral_constant<int, 1>{});
-  ktile(nk - 1, std::integral_constant<int, 2>{});
-  if (wm == 0) lds_barrier();
-  __syncthreads();
-  epilogue_store<BM, BN, NT, TM, TN, EPI>(g, lds, acc, m0, n0, wm * WTM, wn * WTN, tid, fr, fg);
-}
-
-// Register-direct epilogue of the persistent kernel: the arithmetic of epilogue_store + epi8 (first rounding
-// fp16(acc + bias) / fp16(acc), then residual / QuickGELU / QuickGELU' in fp32 and one more fp16 rounding),
-// without the LDS staging pass, so the operand ring stays free for the next tile's first K-steps.  A lane's
-// accumulators hold 4 columns of one row per 16x16 block; the lanes of rows fg and fg ^ 1 (one
-// __shfl_xor(16)) trade halves of two neighbouring blocks so that each lane owns 8 consecutive columns:
-// 16-byte aux loads and stores, a wave instruction covering 16 rows x 64 contiguous bytes.  Needs N % 8 == 0
-// and vec8 (16-byte aligned, 8-element-strided C / aux; the host checks).
-template <int EPI, int TM, int TN>
-MF_DEV void epilogue_regs(const GemmArgs& g, const f32x4 (&acc)[TM][TN], int m0, int n0, int mbase, int nbase, int fr,
-                          int fg) {
-  static_assert(EPI != EPI_F32, "fp32 output: not on the persistent kernel");
-  static_assert(TN % 2 == 0, "block pairs");
-  const bool odd = fg & 1;
-  f16x4 bv[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU)
-      bv[j] = *(const f16x4*)(g.bias + min(n0 + nbase + j * 16 + 4 * fg, g.N - 4));
-    else
-      bv[j] = f16x4{};
-  }
-  constexpr int HM = TM / 2;  // two halves of the rows: a half's aux loads are issued before its first use
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
-    f16x8 auxv[HM][TN / 2];
-    if constexpr (epi_reads_aux<EPI>()) {
-#pragma unroll
-      for (int i = 0; i < HM; ++i) {
-        const int64_t m = m0 + mbase + (hh * HM + i) * 16 + fr;
-#pragma unroll
-        for (int p = 0; p < TN / 2; ++p) {
-          const int n = n0 + nbase + (2 * p + odd) * 16 + 4 * (fg & 2);
-          auxv[i][p] = (m < g.M && n < g.N) ? *(const f16x8*)(g.aux_in + m * g.ld_aux + n) : f16x8{};
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < HM; ++i) {
-      const int64_t m = m0 + mbase + (hh * HM + i) * 16 + fr;
-#pragma unroll
-      for (int p = 0; p < TN / 2; ++p) {
-        f16x4 t[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const f32x4 v = acc[hh * HM + i][2 * p + q];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU)
-              t[q][e] = (f16)(v[e] + (float)bv[2 * p + q][e]);
-            else
-              t[q][e] = (f16)v[e];
-          }
-        }
-        // even rows keep block 2p and take the partner's columns 4..7 of it; odd rows keep block 2p + 1
-        const uint2 send = __builtin_bit_cast(uint2, odd ? t[0] : t[1]);
-        const uint2 recv = {(unsigned)__shfl_xor((int)send.x, 16, 64), (unsigned)__shfl_xor((int)send.y, 16, 64)};
-        const f16x4 r = __builtin_bit_cast(f16x4, recv);
-        const f16x4 lo = odd ? r : t[0], hi = odd ? t[1] : r;
-        const f16x8 tv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const int n = n0 + nbase + (2 * p + odd) * 16 + 4 * (fg & 2);
-        if (m >= g.M || n >= g.N) continue;
-        f16x8 out;
-        if constexpr (EPI == EPI_NONE || EPI == EPI_BIAS) {
-          out = tv;
-        } else if constexpr (EPI == EPI_BIAS_RESID || EPI == EPI_RESID) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) out[e] = (f16)((float)auxv[i][p][e] + (float)tv[e]);
-        } else if constexpr (EPI == EPI_BIAS_GELU) {
-          if (g.aux_out) st16_stream(g.aux_out + m * g.ld_aux + n, tv);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            float t2;
-            out[e] = (f16)quick_gelu16((float)tv[e], &t2);
-          }
-        } else if constexpr (EPI == EPI_DGELU) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) out[e] = (f16)quick_gelu16_bwd((float)tv[e], (float)auxv[i][p][e]);
-        }
-        *(f16x8*)((f16*)g.C + m * g.ldc + n) = out;
-      }
-    }
-  }
-}
-
-// XCD x's block of tile positions in tile_of's order: [off, off + sz)
-MF_DEV void xcd_block(int x, int tiles_m, int tiles_n, int xb, int& off, int& sz) {
-  const int nb = 1 << xb, ma = 8 >> xb;
-  off = 0;
-#pragma unroll 1
-  for (int y = 0; y <= x; ++y) {
-    const int ia = y >> xb, jb = y & (nb - 1);
-    const int s = (tiles_m * (ia + 1) / ma - tiles_m * ia / ma) * (tiles_n * (jb + 1) / nb - tiles_n * jb / nb);
-    if (y == x) sz = s;
-    else off += s;
-  }
-}
-
-// gemm8sp: gemm8s made persistent for products with many rounds of 256x256 tiles (the C5 text tower,
-// M = 77 000).  One workgroup per CU; workgroup (xcd, l) walks the tiles l, l + nl, .. of its XCD's block
-// (tile_of's blocking, nl = workgroups per XCD), so at any time an XCD's workgroups share a few A panels in
-// its L2.  Per tile: the gemm8s main loop unchanged, THIS tile's epilogue from registers (epilogue_regs,
-// no LDS pass), then the NEXT tile's first seven half-tiles into the ring; one vmcnt(0) retires both (no
-// store is outstanding when the next tile's counted ring waits run).  Bit-identical to gemm8s (the same
-// MFMA order per accumulator and the same epilogue arithmetic).  Measured (r03, gemm_bench.py c5,
-// profiles/r03_v6_persistent_gemm.txt): no faster than gemm8s on any C5 product (an apparent +8 % on the
-// in-projection was the benchmark's first-column warm-up: the same tile measured twice in one run gave 668
-// and 714 TFLOP/s).  Where the epilogue writes 2 x 128 KB per tile (c_fc fwd, c_proj dX) the stores of a
-// round set the pace (in-kernel stamps: the epilogue phase grows from 7.7 to 12-13 us when the next tile's
-// loads are in flight beside it; issuing them before the epilogue, or starting every other workgroup 7-20 us
-// late to split the store bursts, was no better).  Kept as the A/B tile 27, not chosen by the heuristic.
-template <int EPI>
-__global__ __launch_bounds__(512) void gemm8sp_kernel(GemmArgs g) {
-  constexpr int BM = 256, BN = 256, WM = 2, WN = 4;
-  constexpr int WTM = BM / WM, WTN = BN / WN, QM = WTM / 2;
-  constexpr int QTM = QM / 16, TN = WTN / 16, TM = 2 * QTM;
-  constexpr int INS = 2;
-  constexpr int HK = 32;
-  constexpr int SLOT = 256 * HK;
-  constexpr int NSLOT = 10, E = 7;
-  static_assert(NSLOT * SLOT * 2 <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(1024))) f16 lds[NSLOT * SLOT];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WN, wn = wid % WN;
-  const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
-  const int xcd = blockIdx.x & 7, l = blockIdx.x >> 3, nl = gridDim.x >> 3;
-  int off, sz;
-  xcd_block(xcd, tiles_m, tiles_n, g.xb, off, sz);
-  if (l >= sz) return;  // uniform over the workgroup
-
-  const int src_chunk = (lane & 3) ^ ((-(lane >> 4)) & 3);
-  const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.A, 0, (int)(((int64_t)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t b_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.B, 0, (int)(((int64_t)(g.N - 1) * g.ldb + g.K) * 2), 0x00020000);
-  const int a_voff = ((lane >> 2) * (int)g.lda + src_chunk * 8) * 2;
-  const int b_voff = ((lane >> 2) * (int)g.ldb + src_chunk * 8) * 2;
-  int m0 = 0, n0 = 0;  // the tile the ring is loading
-  auto set_tile = [&](int j) {
-    int mt, nt;
-    tile_of(off + j, tiles_m, tiles_n, g.xb, mt, nt);
-    m0 = mt * BM;
-    n0 = nt * BN;
-  };
-  auto slot = [&](int h) { return lds + (h % NSLOT) * SLOT; };
-  auto issue = [&](int H) {
-    f16* dst = slot(H);
-    const int kofs = (H >> 2) * BK + HK * ((H >> 1) & 1);
-    if ((H & 1) == 0) {
-#pragma unroll
-      for (int i = 0; i < INS; ++i) {
-        const int row = (wid * INS + i) * 16;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(dst + row * HK), 16,
-                                                 a_voff + (int)(((int64_t)(m0 + row) * g.lda + kofs) * 2), 0, 0, 0);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < INS; ++i) {
-        const int row = (wid * INS + i) * 16;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_ptr_t)(dst + row * HK), 16,
-                                                 b_voff + (int)(((int64_t)(n0 + row) * g.ldb + kofs) * 2), 0, 0, 0);
-      }
-    }
-  };
-
-  f32x4 acc[TM][TN];
-  const int fr = lane & 15, fg = lane >> 4;
-  const int frag_off = fr * HK + ((fg ^ ((-(fr >> 2)) & 3)) << 3);
-  auto read_a = [&](f16x8 (&af)[QTM], const f16* img, int mh) {
-#pragma unroll
-    for (int i = 0; i < QTM; ++i) af[i] = *(const f16x8*)(img + (wm * WTM + mh * QM + i * 16) * HK + frag_off);
-  };
-  auto read_b = [&](f16x8 (&bf)[TN], const f16* img) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) bf[j] = *(const f16x8*)(img + (wn * WTN + j * 16) * HK + frag_off);
-  };
-  auto mma = [&](const f16x8 (&af)[QTM], const f16x8 (&bf)[TN], int mh) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < QTM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[mh * QTM + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[mh * QTM + i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  const int nk = g.K / BK;  // >= 2
-  f16x8 fx[QTM], fy[QTM], fb0[TN], fb1[TN];
-  auto ktile = [&](int kt, auto mode_tag) {  // gemm8s's K-tile, unchanged
-    constexpr int MODE = decltype(mode_tag)::value;
-    const int h0 = 4 * kt;
-    read_a(fx, slot(h0), 0);
-    read_b(fb0, slot(h0 + 1));
-    if constexpr (MODE <= 1) issue(h0 + E);
-    lds_barrier();
-    mma(fx, fb0, 0);
-    lds_barrier();
-    read_a(fy, slot(h0), 1);
-    if constexpr (MODE == 0) issue(h0 + E + 1);
-    if constexpr (MODE == 0) wait_vmcnt<INS * 5>();
-    else if constexpr (MODE == 1) wait_vmcnt<INS * 4>();
-    else wait_vmcnt<0>();
-    lds_barrier();
-    mma(fy, fb0, 1);
-    lds_barrier();
-    read_a(fx, slot(h0 + 2), 1);
-    read_b(fb1, slot(h0 + 3));
-    if constexpr (MODE == 0) issue(h0 + E + 2);
-    lds_barrier();
-    mma(fx, fb1, 1);
-    lds_barrier();
-    read_a(fy, slot(h0 + 2), 0);
-    if constexpr (MODE == 0) issue(h0 + E + 3);
-    if constexpr (MODE == 0) wait_vmcnt<INS * 5>();
-    else if constexpr (MODE == 1) wait_vmcnt<INS * 2>();
-    lds_barrier();
-    mma(fy, fb1, 0);
-    lds_barrier();
-  };
-
-  set_tile(l);
-#pragma unroll
-  for (int h = 0; h < E; ++h) issue(h);
-#pragma unroll 1
-  for (int j = l; j < sz; j += nl) {
-    MF_STAMPI(off + j, 0);
-    const int cm0 = m0, cn0 = n0;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int jj = 0; jj < TN; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    wait_vmcnt<INS * (E - 2)>();  // first tile: half-tiles 0, 1 landed; later tiles: all landed already
-    lds_barrier();
-    MF_STAMPI(off + j, 1);
-    if (wm == 1) lds_barrier();  // the stagger
-    for (int kt = 0; kt < nk - 2; ++kt) ktile(kt, std::integral_constant<int, 0>{});
-    ktile(nk - 2, std::integral_constant<int, 1>{});
-    ktile(nk - 1, std::integral_constant<int, 2>{});
-    if (wm == 0) lds_barrier();  // even out the barrier count
-    __syncthreads();             // every wave is past the ring
-    MF_STAMPI(off + j, 2);
-    epilogue_regs<EPI>(g, acc, cm0, cn0, wm * WTM, wn * WTN, fr, fg);
-    if (j + nl < sz) {
-      set_tile(j + nl);
-#pragma unroll
-      for (int h = 0; h < E; ++h) issue(h);
-    }
-    wait_vmcnt<0>();
-    MF_STAMPI(off + j, 3);
-  }
-}
-
-int launch_tile8sp(const GemmArgs& a, int epi, hipStream_t st) {
-  static const int ncu = [] {
-    int d = 0, n = 0;
-    (void)hipGetDevice(&d);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
-    return n > 0 ? n : 256;
-  }();
-  const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
-  const int grid = std::max(8, std::min(tiles, ncu) / 8 * 8);  // whole XCDs (round-robin placement)
-  if (epi == EPI_F32 || !a.vec8 || (a.N % 8) != 0) return mf_set_error("mf_gemm: persistent tile needs fp16 C, N % 8 == 0", -2);
-  switch (epi) {
-    case EPI_NONE: gemm8sp_kernel<EPI_NONE><<<grid, 512, 0, st>>>(a); break;
-    case EPI_BIAS: gemm8sp_kernel<EPI_BIAS><<<grid, 512, 0, st>>>(a); break;
-    case EPI_BIAS_RESID: gemm8sp_kernel<EPI_BIAS_RESID><<<grid, 512, 0, st>>>(a); break;
-    case EPI_BIAS_GELU: gemm8sp_kernel<EPI_BIAS_GELU><<<grid, 512, 0, st>>>(a); break;
-    case EPI_DGELU: gemm8sp_kernel<EPI_DGELU><<<grid, 512, 0, st>>>(a); break;
-    case EPI_RESID: gemm8sp_kernel<EPI_RESID><<<grid, 512, 0, st>>>(a); break;
-    default: return mf_set_error("mf_gemm_nt: bad epilogue", -2);
-  }
-  MF_CHECK_LAUNCH();
-  return 0;
-}
-
 int launch_tile8s(const GemmArgs& a, int epi, hipStream_t st) {
   const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
   dim3 grid(tiles), block(512);
@@ -1426,24 +988,6 @@ int launch_tile8s(const GemmArgs& a, int epi, hipStream_t st) {
     case EPI_DGELU: gemm8s_kernel<EPI_DGELU><<<grid, block, 0, st>>>(a); break;
     case EPI_F32: gemm8s_kernel<EPI_F32><<<grid, block, 0, st>>>(a); break;
     case EPI_RESID: gemm8s_kernel<EPI_RESID><<<grid, block, 0, st>>>(a); break;
-    default: return mf_set_error("mf_gemm_nt: bad epilogue", -2);
-  }
-  MF_CHECK_LAUNCH();
-  return 0;
-}
-
-template <int BM, int BN>
-int launch_tile8g(const GemmArgs& a, int epi, hipStream_t st) {
-  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  dim3 grid(tiles), block(512);
-  switch (epi) {
-    case EPI_NONE: gemm8g_kernel<BM, BN, EPI_NONE><<<grid, block, 0, st>>>(a); break;
-    case EPI_BIAS: gemm8g_kernel<BM, BN, EPI_BIAS><<<grid, block, 0, st>>>(a); break;
-    case EPI_BIAS_RESID: gemm8g_kernel<BM, BN, EPI_BIAS_RESID><<<grid, block, 0, st>>>(a); break;
-    case EPI_BIAS_GELU: gemm8g_kernel<BM, BN, EPI_BIAS_GELU><<<grid, block, 0, st>>>(a); break;
-    case EPI_DGELU: gemm8g_kernel<BM, BN, EPI_DGELU><<<grid, block, 0, st>>>(a); break;
-    case EPI_F32: gemm8g_kernel<BM, BN, EPI_F32><<<grid, block, 0, st>>>(a); break;
-    case EPI_RESID: gemm8g_kernel<BM, BN, EPI_RESID><<<grid, block, 0, st>>>(a); break;
     default: return mf_set_error("mf_gemm_nt: bad epilogue", -2);
   }
   MF_CHECK_LAUNCH();
@@ -1636,11 +1180,15 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     } else
       tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
   }
-  // tile ids: the ones the heuristic picks (1, 2, 3, 10, 15, 16, 20 = gemm8s, 26, 31, 33), plus 11 (160x128 with a
-  // 3-stage ring), 21 (8-wave 256x128) and 22 (the unstaggered gemm8 at 256x256) as A/B baselines
-  // (tests/diagnostics/gemm_bench.py); the
-  // sweep also covered 128x192, 192x128, 128x160, 160x160, 224x128, 96x192, 64x128, 160x192, 192x192,
-  // 256x128 on 4 waves and 128x256 / 128x128 on 8 waves (slower on every MaPLe shape)
+  // tile ids: the ones the heuristic picks (1, 2, 3, 10, 15, 16, 26, 31, 33, 40 = gemm8f), plus 11 (160x128 with a
+  // 3-stage ring), 20 (gemm8s, the [256][32]-image 256x256 kernel gemm8f replaced in r05), 21 (8-wave 256x128) and
+  // 22 (the unstaggered gemm8 at 256x256) as A/B baselines (tests/diagnostics/gemm_bench.py); the sweep also covered
+  // 128x192, 192x128, 128x160, 160x160, 224x128, 96x192, 64x128, 160x192, 192x192, 256x128 on 4 waves and 128x256 /
+  // 128x128 on 8 waves (slower on every MaPLe shape); r05 (profiles/r05_v2..v4_*): 224x96 / 224x128 / 208x96 4-wave
+  // one-round tiles, 8-wave full-line 160x128 / 192x128 / 128x128 / 96x192 (gemm8g) and a persistent gemm8f whose next
+  // tile's loads precede the current tile's buffer-store epilogue (gemm8fp) -- none faster where it would be picked
+  // (gemm8g 192x128 within +0..2 % on the c4 K >= 2 304 products; gemm8fp +3..+11 % on some C5 products and -4..-60 %
+  // on others), removed
   switch (tile) {
     case 1: return launch_tile<128, 128, 2, 2, 2>(a, epilogue, st);
     case 2: return launch_tile<128, 64, 2, 2, 2>(a, epilogue, st);
@@ -1655,16 +1203,7 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     case 20: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8s(a, epilogue, st);
     case 21: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 2, 4>(a, epilogue, st);
     case 22: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 256, 2, 4>(a, epilogue, st);
-    case 41: return launch_tile<224, 96, 2, 2, 2>(a, epilogue, st);
-    case 42: return launch_tile<224, 96, 2, 2, 3>(a, epilogue, st);
-    case 43: return launch_tile<224, 128, 2, 2, 3>(a, epilogue, st);
-    case 44: return launch_tile<208, 96, 1, 2, 3>(a, epilogue, st);
-    case 45: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8g<160, 128>(a, epilogue, st);
-    case 46: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8g<192, 128>(a, epilogue, st);
-    case 47: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8g<128, 128>(a, epilogue, st);
-    case 48: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8g<96, 192>(a, epilogue, st);
     case 40: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8f(a, epilogue, st);
-    case 27: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8sp(a, epilogue, st);
     default: return mf_set_error("mf_gemm: bad tile id", -2);
   }
 }

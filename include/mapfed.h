@@ -32,8 +32,8 @@ int mf_abi_version(void);
  *           backward's operand; null: not stored, the forward-only eval engine), C = QuickGELU | 4 C = QuickGELU'(fp16(acc), aux_in) | 5 fp32 store | 6 +aux_in residual
  * tile: 0 auto (latency picks), -1 auto for a product of the tower off the step's critical path (tiles chosen for
  *       work per CU-second; the engine passes it for the text tower at c4, the vision tower at C5), 1 128x128,
- *       2 128x64, 3 64x64, 10 160x128, 15 96x128, 16 160x64, 20 256x256 8-wave, 26 96x64, 27 persistent 256x256,
- *       40 256x256 8-wave full-line (gemm8f), 45-48 8-wave full-line 160x128 / 192x128 / 128x128 / 96x192.
+ *       2 128x64, 3 64x64, 10 160x128, 15 96x128, 16 160x64, 20 256x256 8-wave, 26 96x64, 40 256x256 8-wave
+ *       full-line (gemm8f).
  * Replaces: nn.Linear / addmm inside nn.MultiheadAttention in_proj + out_proj, mlp.c_fc, QuickGELU,
  * mlp.c_proj and the residual adds (clip/model.py:274-280,303-305,350-351), the patch-embed conv as
  * im2col GEMM (clip/model.py:514), the tower heads (clip/model.py:570, trainers/maple.py:76) and all

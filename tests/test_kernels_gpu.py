@@ -44,11 +44,12 @@ def test_gemm8_staggered_matches_unstaggered(dev, M, N, K):
     assert torch.equal(C20, C22)
 
 
-@pytest.mark.parametrize("M,N,K", [(33000, 1024, 192), (77000, 2048, 512), (20001, 512, 128), (30000, 760, 128)])
-def test_gemm8_persistent_matches_staggered(dev, M, N, K):
-    """The persistent 256x256 kernel (tile 27: every workgroup walks several tiles, the next tile's first
-    K-steps land under the register-direct epilogue) against gemm8s (tile 20): bit-identical for every fp16
-    epilogue, ragged M included."""
+@pytest.mark.parametrize("M,N,K", [(33000, 1024, 192), (77000, 2048, 512), (20001, 512, 128), (30000, 760, 128),
+                                   (20001, 2304, 768), (1000, 256, 192), (6368, 2304, 768)])
+def test_gemm8_fullline_matches_staggered(dev, M, N, K):
+    """The full-line 256x256 kernel gemm8f (tile 40: [128 rows][64 k] half-tiles) against gemm8s (tile 20: [256
+    rows][32 k]) -- bit-identical for every fp16 epilogue, ragged M / N included, and the pre-activation store
+    skipped (aux_out null, the forward-only engine) without changing C."""
     g = torch.Generator(device="cpu").manual_seed(M + K)
     A = torch.randn(M, K, generator=g).half().to(dev)
     B = (torch.randn(N, K, generator=g) * K ** -0.5).half().to(dev)
@@ -57,15 +58,19 @@ def test_gemm8_persistent_matches_staggered(dev, M, N, K):
     for epi in (ops.EPI_NONE, ops.EPI_BIAS, ops.EPI_BIAS_RESID, ops.EPI_BIAS_GELU, ops.EPI_DGELU, ops.EPI_RESID):
         kw = {"bias": b} if epi in (ops.EPI_BIAS, ops.EPI_BIAS_RESID, ops.EPI_BIAS_GELU) else {}
         outs = []
-        for tile in (20, 27):
+        for tile in (20, 40):
             aux_out = torch.empty(M, N, device=dev, dtype=torch.float16) if epi == ops.EPI_BIAS_GELU else None
             aux_in = R if epi in (ops.EPI_BIAS_RESID, ops.EPI_DGELU, ops.EPI_RESID) else None
             C = ops.gemm_nt(A, B, aux_in=aux_in, aux_out=aux_out, epilogue=epi, tile=tile, **kw)
             outs.append((C, aux_out))
+        if epi == ops.EPI_BIAS_GELU:  # the forward-only engine's form: no pre-activation store
+            for tile in (20, 40):
+                outs.append((ops.gemm_nt(A, B, epilogue=epi, tile=tile, **kw), None))
         torch.cuda.synchronize()
-        assert torch.equal(outs[0][0], outs[1][0]), f"epilogue {epi}"
-        if epi == ops.EPI_BIAS_GELU:
-            assert torch.equal(outs[0][1], outs[1][1])
+        for k, (C, aux_out) in enumerate(outs[1:], 1):
+            assert torch.equal(outs[0][0], C), f"epilogue {epi}, variant {k}"
+            if aux_out is not None:
+                assert torch.equal(outs[0][1], aux_out), f"epilogue {epi}, variant {k} (pre-activation)"
 
 
 @pytest.mark.parametrize("M,N,K,epi", [(2926, 512, 2048, 2), (2926, 1536, 512, 1), (6368, 768, 3072, 0),
@@ -107,7 +112,10 @@ def test_gemm_side_tower_tile_hint_is_bit_identical(dev, M, N, K, epi):
                                         (97, 200, 64, 15), (161, 72, 128, 16), (100, 76, 192, 26),
                                         # the small clients' 4-stage rings (tiles 31, 33)
                                         (796, 768, 3072, 31), (770, 512, 2048, 33), (100, 72, 320, 31),
-                                        (33, 136, 192, 33)])
+                                        (33, 136, 192, 33),
+                                        # the full-line 8-wave 256x256 tile (gemm8f, 40)
+                                        (6368, 2304, 768, 40), (1000, 760, 192, 40), (129, 260, 128, 40),
+                                        (20001, 2304, 768, 40), (300, 516, 192, 40)])
 def test_gemm_bias(dev, M, N, K, tile):
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g).half().to(dev)
