@@ -26,7 +26,8 @@ Two exchange modes (FED.AGGREGATION in the trainer config):
     the fp32 summation order is the reference's torch.stack(...) order, so the fp16 result is
     bit-identical to safe_average_weights at any world size (CPU-torch mean semantics: sum then divide,
     which tests/golden/fedavg.npz pins).  On a GPU the chain runs on a side stream (all_to_all -> reduce
-    -> all_gather), so start() returns at once and the caller's next kernels run under it.
+    -> all_gather), so start() returns at once and the caller's next kernels run under it; under gloo (the
+    world-size-2 CPU tests) the same _ordered_chain runs with host waits, so those tests cover its code.
   * "allreduce": the rank's buckets summed in client order, then one RCCL all_reduce(SUM).  The same
     traffic, but RCCL's ring order changes the fp32 summation order per chunk; with three or more ranks the
     fp16-rounded result can differ from the reference's in the last fp16 bit of rare elements.
@@ -206,7 +207,6 @@ class FedAvgExchange:
                 self.side = torch.cuda.Stream(device=dev)
         self.started = False
         self.work = None
-        self.pending_a2a = None
 
     def _send_image(self) -> torch.Tensor:
         if self.C == 1:
@@ -227,7 +227,7 @@ class FedAvgExchange:
     def start(self):
         """Launch the exchange of the packed buckets (asynchronously where the backend allows)."""
         self.started = True
-        self.work = self.pending_a2a = None
+        self.work = None
         if not self.distributed:
             return  # one process: the sum is formed in finish()
         if not self.sharded:
@@ -241,27 +241,30 @@ class FedAvgExchange:
             # the whole chain on the side stream: the current stream only waits for it in finish()
             self.side.wait_stream(torch.cuda.current_stream(send.device))
             with torch.cuda.stream(self.side):
-                a2a = dist.all_to_all_single(self.recv, send, group=self.group, async_op=True)
-                a2a.wait()  # a stream dependency, not a host wait
-                self.k.fedavg_reduce_ordered(self.recv, self.world * self.C, self.shard)
-                self.work = dist.all_gather_into_tensor(self.total, self.shard, group=self.group, async_op=True)
-        else:  # gloo: reduce and gather in finish()
-            src = send.cpu() if self.host_stage else send
-            self.recv_x = torch.empty_like(src)
-            self.pending_a2a = dist.all_to_all_single(self.recv_x, src, group=self.group, async_op=True)
+                self.work = self._ordered_chain(send)
+        else:  # gloo: the same chain, its waits host waits
+            self.work = self._ordered_chain(send)
+
+    def _ordered_chain(self, send: torch.Tensor):
+        """all_to_all of the shards -> client-ordered sum of this rank's shard -> all_gather of the sums.
+        One code path for every backend: under RCCL (on the side stream) a2a.wait() is a stream dependency;
+        under gloo it is a host wait, and with device buckets (host_stage) the collectives move host copies.
+        Returns the all_gather's work handle (None when it completed here)."""
+        hs = self.host_stage
+        recv = torch.empty(self.recv.numel(), dtype=torch.float32) if hs else self.recv
+        a2a = dist.all_to_all_single(recv, send.cpu() if hs else send, group=self.group, async_op=True)
+        a2a.wait()
+        if hs:
+            self.recv.copy_(recv)
+        self.k.fedavg_reduce_ordered(self.recv, self.world * self.C, self.shard)
+        if hs:
+            out = torch.empty(self.total.numel(), dtype=torch.float32)
+            dist.all_gather_into_tensor(out, self.shard.cpu(), group=self.group)
+            self.total.copy_(out)
+            return None
+        return dist.all_gather_into_tensor(self.total, self.shard, group=self.group, async_op=True)
 
     def _complete(self):
-        if self.pending_a2a is not None:
-            self.pending_a2a.wait()
-            self.pending_a2a = None
-            self.recv.copy_(self.recv_x)
-            self.k.fedavg_reduce_ordered(self.recv, self.world * self.C, self.shard)
-            if self.host_stage:
-                out = torch.empty(self.total.numel(), dtype=torch.float32)
-                dist.all_gather_into_tensor(out, self.shard.cpu(), group=self.group)
-                self.total.copy_(out)
-            else:
-                dist.all_gather_into_tensor(self.total, self.shard, group=self.group)
         if self.work is not None:
             self.work.wait()
             self.work = None
