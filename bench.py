@@ -160,8 +160,8 @@ def side_config(name, dev, world, rank, steps=5, warmup=2, seed=0, eot_truncate=
         out.update(text_tokens=Lt, executed_gflop_per_step=exec_flop / 1e9,
                    algorithmic_gflop_per_step=step_flop / 1e9,
                    flop_basis="model_tflops / model_mfma_frac: executed FLOP (text tower on text_tokens rows)",
-                   parity="logits and loss bit-identical to the 77-token tower; gradients equal up to fp32 summation "
-                          "order (tests/test_engine_gpu.py::test_eot_truncated_text_tower_matches_full)")
+                   parity="bit-identical to the 77-token tower: logits, loss, every gradient and the updated "
+                          "weights (tests/test_engine_gpu.py::test_eot_truncated_text_tower_matches_full)")
     del g, e
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -366,8 +366,14 @@ def main():
                     "flop_basis": "model_tflops / model_mfma_frac: executed FLOP (text tower on text_tokens rows)",
                     "executed_gflop_per_step": exec_flop_t / 1e9,
                     "algorithmic_gflop_per_step": (B * FLOP_PER_IMAGE + K * FLOP_PER_CLASS) / 1e9,
-                    "parity": "logits and loss bit-identical to the 77-token tower; gradients equal up to fp32 "
-                              "summation order (tests/test_engine_gpu.py::test_eot_truncated_text_tower_matches_full)"}
+                    "parity": "bit-identical to the 77-token tower: logits, loss, every gradient and the updated "
+                              "weights (tests/test_engine_gpu.py::test_eot_truncated_text_tower_matches_full); the "
+                              "backward's row reductions run over the 77-row layout (mf_layernorm_bwd_live, "
+                              "mf_seq_scatter)",
+                    # live check: this run and the `value` run took the same steps from the same seed and batches
+                    "weights_equal_value_run": bool(torch.equal(eng.flat16, eng_t.flat16)
+                                                    and torch.equal(eng.flat32, eng_t.flat32)
+                                                    and eng.loss() == eng_t.loss())}
         del graph_t, eng_t, fed_t
         torch.cuda.synchronize()
 

@@ -59,6 +59,8 @@ SIGNATURES = {
     "mf_fedavg_reduce_ordered": [P, I, L, L, P, P],
     "mf_seq_grow": [P, P, P, P, I, I, I, I, I, P],
     "mf_seq_grow_bwd": [P, P, I, I, I, I, I, P],
+    "mf_seq_scatter": [P, L, P, L, I, I, I, I, P],
+    "mf_layernorm_bwd_live": [P, L, P, L, P, P, P, P, L, P, L, P, I, I, I, I, P, I, I, P],
     "mf_caption_pool": [P, I, I, P, I, P, I, P, P],
     "mf_nonfinite_flag": [P, L, I, P, P],
     "mf_augment_ws_bytes": [I, I, I, I],

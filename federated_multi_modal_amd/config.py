@@ -185,9 +185,10 @@ def extend_cfg(cfg: CfgNode) -> None:
     cfg.TRAINER.COOP = CfgNode(dict(N_CTX=16, CSC=False, CTX_INIT="", PREC="fp16", CLASS_TOKEN_POSITION="end"))
     cfg.TRAINER.COCOOP = CfgNode(dict(N_CTX=16, CTX_INIT="", PREC="fp16"))
     # EOT_TRUNCATE (MI355X addition, off by default): run the text tower on the first max(EOT) + 1 tokens
-    # only.  The causal mask makes every later position dead for the EOT features, so logits and loss are
-    # bit-identical (tests/test_engine_gpu.py::test_eot_truncated_text_tower_matches_full); gradients agree
-    # up to fp32 summation order (the GEMM tiles follow the smaller row count).
+    # only.  The causal mask makes every later position dead for the EOT features and gives it an exactly zero
+    # gradient; the truncated tower runs its backward's row reductions over the 77-row layout, so logits, loss,
+    # every gradient and the updated weights are bit-identical to the full tower's
+    # (tests/test_engine_gpu.py::test_eot_truncated_text_tower_matches_full).
     # EVAL_GROUP (MI355X addition): test() feeds this many TEST.BATCH_SIZE loader batches to one forward of a
     # forward-only engine.  Every product accumulates each output in the same k order whatever the tile, and
     # every other kernel is per row / per head, so a row's logits do not depend on the batch it is in

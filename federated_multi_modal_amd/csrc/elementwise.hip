@@ -678,3 +678,31 @@ extern "C" int mf_small_linear_bwd_batch(const void* descs, int n, int max_m, in
   MF_CHECK_LAUNCH();
   return 0;
 }
+
+namespace {
+__global__ void seq_scatter_kernel(const f16* __restrict__ src, int64_t ld_src, f16* __restrict__ dst, int64_t ld_dst,
+                                   int L_live, int L_full, int C8, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int64_t row = i / C8;
+  const int c = (int)(i % C8) * 8;
+  const int64_t n = row / L_live, t = row % L_live;
+  *(f16x8*)(dst + (n * L_full + t) * ld_dst + c) = *(const f16x8*)(src + row * ld_src + c);
+}
+}  // namespace
+
+// Rows of N compact L_live-row sequences into the first L_live rows of N L_full-row sequences (dst row
+// n * L_full + t = src row n * L_live + t; dst's other rows untouched).  The EOT-truncated text tower's operands
+// of its block-11 weight gradients, laid out as the full-length tower's (whose extra rows are zero).
+extern "C" int mf_seq_scatter(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, int N, int L_live,
+                              int L_full, int C, void* stream) {
+  if (N <= 0 || C <= 0) return 0;
+  if (L_live <= 0 || L_live > L_full || C % 8 || ld_src % 8 || ld_dst % 8 || ld_src < C || ld_dst < C ||
+      (uintptr_t)src % 16 || (uintptr_t)dst % 16)
+    return mf_set_error("mf_seq_scatter: bad shape or alignment", -1);
+  const int64_t total = (int64_t)N * L_live * (C / 8);
+  seq_scatter_kernel<<<nblk(total), 256, 0, (hipStream_t)stream>>>((const f16*)src, ld_src, (f16*)dst, ld_dst, L_live,
+                                                                  L_full, C / 8, total);
+  MF_CHECK_LAUNCH();
+  return 0;
+}

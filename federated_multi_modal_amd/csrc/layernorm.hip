@@ -286,7 +286,12 @@ __global__ __launch_bounds__(HWB * 32) void ln_bwd2_kernel(const f16* __restrict
                                                      int64_t ldres, f16* dx, int64_t lddx,
                                                      float* __restrict__ dg_part, float* __restrict__ db_part,
                                                      int rows, float* __restrict__ inj_part = nullptr,
-                                                     int inj_L = 1, int inj_row0 = 0, int inj_n = 0) {
+                                                     int inj_L = 1, int inj_row0 = 0, int inj_n = 0,
+                                                     int seg_live = 0, int seg_full = 0) {
+  // seg_full > 0: `rows` counts VIRTUAL rows of seg_full-row sequences, of which the first seg_live of each are
+  // stored (compact row (v / seg_full) * seg_live + v % seg_full); the rest are rows whose dy is exactly zero
+  // (the text tower's tokens after every class's EOT, mf_layernorm_bwd_live): they are not read and add nothing,
+  // so the row blocks, and with them the dgamma / dbeta partials, are those of the full-length tower
   constexpr int CH = D / 256;
   static_assert(HWB == 8 || HWB == 16, "half-waves per block");
   constexpr int RPH = LN_ROWS_PER_BLOCK / HWB;  // rows per half-wave
@@ -311,11 +316,19 @@ __global__ __launch_bounds__(HWB * 32) void ln_bwd2_kernel(const f16* __restrict
   const int r0 = blockIdx.x * LN_ROWS_PER_BLOCK + hw * RPH;
   f16x8 tx[RPH][CH], td[RPH][CH], tr[RPH][CH];
   int srcs[RPH];
+  bool use[RPH];
   float means[RPH], rstds[RPH];
 #pragma unroll
   for (int k = 0; k < RPH; ++k) {
-    const int row = min(r0 + k, rows - 1);
+    int row = min(r0 + k, rows - 1);
+    use[k] = r0 + k < rows;
+    if (seg_full > 0) {
+      const int t = row % seg_full;
+      use[k] = use[k] && t < seg_live;
+      row = use[k] ? (row / seg_full) * seg_live + t : 0;
+    }
     srcs[k] = ridx ? ridx[row] : row;
+    if (seg_full > 0 && !use[k]) continue;  // a zero-gradient row: nothing to read
     means[k] = mean_in[row];
     rstds[k] = rstd_in[row];
 #pragma unroll
@@ -328,7 +341,7 @@ __global__ __launch_bounds__(HWB * 32) void ln_bwd2_kernel(const f16* __restrict
   }
 #pragma unroll
   for (int k = 0; k < RPH; ++k) {
-    if (r0 + k < rows) {
+    if (use[k]) {
       const float mean = means[k], rstd = rstds[k];
       float sdg0 = 0.f, sdg1 = 0.f, sdgx0 = 0.f, sdgx1 = 0.f;  // ln_bwd_kernel's order (see ln_fwd2_kernel)
 #pragma unroll
@@ -591,6 +604,44 @@ extern "C" int mf_layernorm_bwd_inject(const void* dy, int64_t lddy, const void*
     ln_bwd2_kernel<512><<<nblk, 256, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, nullptr, gamma, mean, rstd,
                                               (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows, inj_part,
                                               L, row0, nrows);
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
+// LayerNorm backward (partials only) of a tower that stores only the first L_live rows of each of its `seqs`
+// L_full-row sequences (the EOT-truncated text tower: rows past every class's EOT have exactly zero gradient and
+// are not computed).  The compact rows (seqs * L_live, row n * L_live + t) are processed as the rows t < L_live of
+// the full-length tower: the row blocks, the block partials (workspace: 2 * mf_layernorm_bwd_blocks(seqs * L_full)
+// * D floats) and so the dgamma / dbeta that mf_col_reduce_batch forms from them are bit for bit those of
+// mf_layernorm_bwd over the full tower, whose extra rows add zeros.  inj_part (optional): the deep-prompt
+// injection backward of mf_layernorm_bwd_inject, rows row0 .. row0 + nrows - 1 of each sequence.
+extern "C" int mf_layernorm_bwd_live(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* gamma,
+                                     const float* mean, const float* rstd, const void* dres, int64_t ldres, void* dx,
+                                     int64_t lddx, float* workspace, int seqs, int L_live, int L_full, int D,
+                                     float* inj_part, int row0, int nrows, void* stream) {
+  if (seqs <= 0) return 0;
+  if (D != 512 && D != 768) return mf_set_error("mf_layernorm_bwd_live: D must be 512 or 768", -1);
+  if (L_live <= 0 || L_live > L_full) return mf_set_error("mf_layernorm_bwd_live: 0 < L_live <= L_full", -1);
+  if (inj_part && (row0 < 0 || row0 + nrows > L_live)) return mf_set_error("mf_layernorm_bwd_live: prompt rows", -1);
+  const bool v16 = ((uintptr_t)dy % 16 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)dx % 16 == 0) &&
+                   (!dres || ((uintptr_t)dres % 16 == 0 && ldres % 8 == 0)) && lddy % 8 == 0 && ldx % 8 == 0 &&
+                   lddx % 8 == 0 && (uintptr_t)inj_part % 16 == 0;
+  if (!v16) return mf_set_error("mf_layernorm_bwd_live: needs 16-byte aligned rows", -1);
+  const int rows = seqs * L_full;  // virtual
+  const int nblk = mf_layernorm_bwd_blocks(rows);
+  float* dg_part = workspace;
+  float* db_part = workspace + (int64_t)nblk * D;
+  const int inj_n = inj_part ? nrows : 0;
+  hipStream_t st = (hipStream_t)stream;
+#define MF_LN_LIVE(DD, HW, TH)                                                                                       \
+  ln_bwd2_kernel<DD, HW><<<nblk, TH, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, nullptr, gamma, mean, rstd, \
+                                              (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows,     \
+                                              inj_part, L_live, row0, inj_n, L_live, L_full)
+  if (D == 768 && ln_bwd_wide(nblk)) MF_LN_LIVE(768, 16, 512);
+  else if (D == 768) MF_LN_LIVE(768, 8, 256);
+  else if (ln_bwd_wide(nblk)) MF_LN_LIVE(512, 16, 512);
+  else MF_LN_LIVE(512, 8, 256);
+#undef MF_LN_LIVE
   MF_CHECK_LAUNCH();
   return 0;
 }

@@ -51,9 +51,11 @@ class EngineConfig:
     max_grad_norm: float = 1.0
     # Run the text tower on the first max(EOT)+1 tokens instead of all 77 (SURVEY.md §8(d) optional
     # mode, reported separately).  Under the causal mask a token only sees earlier ones, and the tower's
-    # output is gathered at the EOT row, so the dropped tokens cannot reach the loss: the forward is
-    # bit-identical, the backward differs only in fp32 summation order (zero rows fewer in the weight
-    # gradients' reductions).  Off by default: the reference computes all 77.
+    # output is gathered at the EOT row, so the dropped tokens cannot reach the loss and their gradients are
+    # exactly zero.  The truncated tower runs its backward's row reductions (LayerNorm dgamma / dbeta, block
+    # 11's dW and db) over the 77-row layout with zero rows in the dropped places (_Tower.live), so logits,
+    # loss, every gradient and the updated weights are bit-identical to the full tower's.  Off by default: the
+    # reference computes all 77, and the headline bench keeps its work.
     eot_truncate: bool = False
     # The caption-conditioned visual prompts (captions.py, clip/model.py:550-561): the vision tower's
     # prompted blocks each append the batch's B projected caption rows, so block i runs 199 + i*B rows.
@@ -253,8 +255,13 @@ class _Tower:
     (mf_seq_grow_bwd, the prompt's gradient reduced over the sequences)."""
 
     def __init__(self, eng: "MapleEngine", name: str, N: int, L: int, D: int, H: int, layers: int,
-                 causal: bool, inject_row0: int, Ls: Optional[List[int]] = None, ncap: int = 0):
+                 causal: bool, inject_row0: int, Ls: Optional[List[int]] = None, ncap: int = 0,
+                 L_full: Optional[int] = None):
         self.e, self.name, self.N, self.L, self.D, self.H = eng, name, N, L, D, H
+        # L_full (the EOT-truncated text tower): the tower computes only the first L of every L_full-row sequence;
+        # the row reductions of its backward (LayerNorm dgamma / dbeta, block 11's dW and db) run over the
+        # L_full-row layout with zero rows in the other places, so every result is bit for bit the full tower's
+        self.live = (L, L_full) if L_full is not None and L_full != L else None
         self.layers, self.causal, self.row0 = layers, causal, inject_row0
         self.Ls = list(Ls) if Ls is not None else [L] * layers
         assert len(self.Ls) == layers and self.Ls[0] == L
@@ -317,14 +324,19 @@ class _Tower:
         self.tile = 0
         # this tower's LayerNorm dgamma/dbeta partials, reduced in one launch at the end of its backward
         self.lnb = ops.LNGradBatch(dev)
-        self.cs_ws = e(ops.colsum_ws_floats(R, 4 * D), dt=F32)
+        self.cs_ws = e(ops.colsum_ws_floats(R if self.live is None else N * self.live[1], 4 * D), dt=F32)
         # split-K weight gradients of the trainable block (few output tiles, K = R tokens): fp32 partial
         # planes, summed in a fixed order (only where the automatic split count exceeds 1: few 128x128 output tiles)
         shapes = ((3 * D, D), (D, D), (4 * D, D), (D, 4 * D))
-        Rl = Rs[-1]
+        Rl = Rs[-1] if self.live is None else N * self.live[1]
         ws = {s: ops.gemm_splitk_ws_floats(s[0], s[1], Rl) for s in shapes}
         self.dw_split = {s for s in shapes if ws[s] > s[0] * s[1]}
         self.dw_ws = e(max(ws[s] for s in self.dw_split), dt=F32) if self.dw_split else None
+        # the live tower's block-11 dW / db operands in the full row layout (rows past L stay zero: written once)
+        self.full_dy = self.full_x = None
+        if self.live is not None:
+            z = lambda: torch.zeros(Rl, 4 * D, device=dev, dtype=F16)
+            self.full_dy, self.full_x = z(), z()
 
     def _alloc_forward_only(self, e, R, N, H, D, layers):
         """Inference buffers: block i reads X[i] and writes X[i + 1], so two alternating activation buffers
@@ -394,7 +406,13 @@ class _Tower:
         # self.H1 / H2 / G now hold the last layer's (block 11) tensors, kept for its dW
 
     def _dw(self, dY: torch.Tensor, Xin: torch.Tensor, dW: torch.Tensor, db: torch.Tensor):
-        """dW[out,in] = dY^T . Xin (fp16 out; both operands read K-major in place, K = rows), db = colsum(dY)."""
+        """dW[out,in] = dY^T . Xin (fp16 out; both operands read K-major in place, K = rows), db = colsum(dY).
+        A live (EOT-truncated) tower first scatters both operands into the full row layout, so K and the
+        summation order are the full tower's (its extra rows contribute exact zeros)."""
+        if self.live is not None:
+            Ll, Lf = self.live
+            dY = ops.seq_scatter(dY, self.full_dy[:, :dY.shape[1]], self.N, Ll, Lf)[:self.N * Lf]
+            Xin = ops.seq_scatter(Xin, self.full_x[:, :Xin.shape[1]], self.N, Ll, Lf)[:self.N * Lf]
         if tuple(dW.shape) in self.dw_split:
             ops.gemm_splitk(dY, Xin, dW, self.dw_ws, a_kmajor=True, b_kmajor=True)
         else:
@@ -423,7 +441,7 @@ class _Tower:
             if trainable_w:
                 self._dw(dF, self.H2[:R], self.g(i, "mlp.c_fc.weight"), self.g(i, "mlp.c_fc.bias"))
             self.lnb.bwd(dH, self.X1[i], self.p(i, "ln_2.weight"), self.mean2[i], self.rstd2[i], dX,
-                         self.g(i, "ln_2.weight"), self.g(i, "ln_2.bias"), dres=dX)
+                         self.g(i, "ln_2.weight"), self.g(i, "ln_2.bias"), dres=dX, live=self.live)
             # ---- attention: X1 = X + out_proj(attn(ln_1(X)))
             ops.gemm_nt(dX, self.wt(i, "attn.out_proj.weight"), dO, epilogue=ops.EPI_NONE, tile=self.tile)
             if trainable_w:
@@ -437,10 +455,10 @@ class _Tower:
                 # ln_1 backward + the deep prompt's gradient (its rows of dX) in one pass
                 self.lnb.bwd_inject(dH, self.X[i], self.p(i, "ln_1.weight"), self.mean1[i], self.rstd1[i], dX,
                                     self.g(i, "ln_1.weight"), self.g(i, "ln_1.bias"), dX, prompt_grads[i - 1], L,
-                                    self.row0, N_CTX)
+                                    self.row0, N_CTX, live=self.live)
             else:
                 self.lnb.bwd(dH, self.X[i], self.p(i, "ln_1.weight"), self.mean1[i], self.rstd1[i], dX,
-                             self.g(i, "ln_1.weight"), self.g(i, "ln_1.bias"), dres=dX)
+                             self.g(i, "ln_1.weight"), self.g(i, "ln_1.bias"), dres=dX, live=self.live)
             if self.grow[i]:
                 # the block's input was [previous output minus its last n_ctx rows | captions | prompt]: the
                 # prompt's gradient is its rows summed over the sequences; the previous output gets the rest
@@ -504,7 +522,7 @@ class MapleEngine:
         self.vis = _Tower(self, "image_encoder", self.B, self.Lv, d.vision_width, d.vision_heads, d.vision_layers,
                           False, G2 + 1, Ls=Ls, ncap=self.B if cfg.captions else 0)
         self.txt = _Tower(self, "text_encoder", self.K, self.text_len, d.text_width, d.text_heads, d.text_layers,
-                          True, 1)
+                          True, 1, L_full=d.context_length)
         self._build_io()
         # the tower with less projection work per step runs beside the other one (the text tower at c4, the
         # vision tower at C5): its GEMMs take the work-per-CU-second tiles (csrc/gemm.hip, tile -1)

@@ -244,7 +244,11 @@ class LNGradBatch:
         self.dev_descs = None
         self.max_cols = 0
 
-    def bwd(self, dy, x, gamma, mean, rstd, dx, dgamma, dbeta, dres=None, row_index=None):
+    def bwd(self, dy, x, gamma, mean, rstd, dx, dgamma, dbeta, dres=None, row_index=None, live=None):
+        """live = (L_live, L_full): dy / x / dx are the first L_live rows of each L_full-row sequence of a tower
+        whose other rows have zero gradient (mf_layernorm_bwd_live: the full tower's partials)."""
+        if live is not None:
+            return self._bwd_live(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, dres, live, None, 0, 0)
         rows, D = dy.shape
         key = dgamma.data_ptr()
         if key not in self.ws:
@@ -264,10 +268,54 @@ class LNGradBatch:
         _rec(ev)
         return dx
 
-    def bwd_inject(self, dy, x, gamma, mean, rstd, dx, dgamma, dbeta, dres, prompt_grad, L, row0, nrows):
+    def _ws_for(self, dgamma, dbeta, rows, D):
+        key = dgamma.data_ptr()
+        if key not in self.ws:
+            nblk = call("mf_layernorm_bwd_blocks", rows)
+            w = torch.empty(2 * nblk * D, device=self.device, dtype=torch.float32)
+            self.ws[key] = w
+            self.descs.append((w.data_ptr(), dgamma.data_ptr(), nblk, D))
+            self.descs.append((w.data_ptr() + 4 * nblk * D, dbeta.data_ptr(), nblk, D))
+            self.max_cols = max(self.max_cols, D)
+            self.dev_descs = None
+        return self.ws[key]
+
+    def _inj_ws_for(self, prompt_grad, n, nrows, D):
+        ikey = ("inj", prompt_grad.data_ptr())
+        if ikey not in self.ws:
+            part = torch.empty(n * nrows * D, device=self.device, dtype=torch.float32)
+            self.ws[ikey] = part
+            self.descs.append((part.data_ptr(), prompt_grad.data_ptr(), n, nrows * D))
+            self.max_cols = max(self.max_cols, nrows * D)
+            self.dev_descs = None
+        return self.ws[ikey]
+
+    def _bwd_live(self, dy, x, gamma, mean, rstd, dx, dgamma, dbeta, dres, live, prompt_grad, row0, nrows):
+        L_live, L_full = live
+        rows, D = dy.shape
+        assert rows % L_live == 0 and L_live <= L_full
+        seqs = rows // L_live
+        ws = self._ws_for(dgamma, dbeta, seqs * L_full, D)
+        inj = None
+        if prompt_grad is not None:
+            assert prompt_grad.dtype == torch.float32 and prompt_grad.is_contiguous()
+            inj = self._inj_ws_for(prompt_grad, seqs, nrows, D)
+        ev = _hbm(f"layernorm_bwd/D{D}", rows * D * (6.0 + (2.0 if dres is not None else 0.0)) + rows * 8.0
+                  + (ws.numel() + (inj.numel() if inj is not None else 0)) * 4.0)
+        call("mf_layernorm_bwd_live", _p(dy), _ld(dy), _p(x), _ld(x), _p(gamma), _p(mean), _p(rstd), _p(dres),
+             _ld(dres) if dres is not None else 0, _p(dx), _ld(dx), _p(ws), seqs, L_live, L_full, D, _p(inj), row0,
+             nrows, _s())
+        _rec(ev)
+        return dx
+
+    def bwd_inject(self, dy, x, gamma, mean, rstd, dx, dgamma, dbeta, dres, prompt_grad, L, row0, nrows, live=None):
         """bwd() with the deep-prompt injection backward of the same rows fused in
         (mf_layernorm_bwd_inject): prompt_grad (fp32 [nrows, D]) = sum over sequences of those rows' dx,
-        reduced in finish() with the LayerNorm partials; the rows of dx are zeroed."""
+        reduced in finish() with the LayerNorm partials; the rows of dx are zeroed.  live: see bwd() (then
+        L must be its L_live)."""
+        if live is not None:
+            assert L == live[0]
+            return self._bwd_live(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, dres, live, prompt_grad, row0, nrows)
         rows, D = dy.shape
         assert prompt_grad.dtype == torch.float32 and prompt_grad.is_contiguous() and prompt_grad.numel() == nrows * D
         key = dgamma.data_ptr()
@@ -406,6 +454,16 @@ def seq_grow(src, dst, cap, prompt, N, Lp, ncap, n_ctx, D):
     """dst [N*(Lp+ncap), D] = per sequence: src rows [0, Lp-n_ctx) | cap [ncap, D] | fp16(prompt [n_ctx, D])."""
     assert src.shape[0] == N * Lp and dst.shape[0] == N * (Lp + ncap) and prompt.dtype == torch.float32
     call("mf_seq_grow", _p(src), _p(dst), _p(cap), _p(prompt), N, Lp, ncap, n_ctx, D, _s())
+
+
+def seq_scatter(src, dst, N, L_live, L_full):
+    """dst rows n*L_full + t = src rows n*L_live + t (t < L_live), src's columns; dst's other rows untouched."""
+    C = src.shape[1]
+    assert src.shape[0] == N * L_live and dst.shape[0] >= N * L_full and dst.shape[1] >= C
+    ev = _hbm("seq_scatter", 4.0 * N * L_live * C)
+    call("mf_seq_scatter", _p(src), _ld(src), _p(dst), _ld(dst), N, L_live, L_full, C, _s())
+    _rec(ev)
+    return dst
 
 
 def seq_grow_bwd(ddst, dsrc, N, Lp, ncap, n_ctx, D):

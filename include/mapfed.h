@@ -88,6 +88,17 @@ int mf_layernorm_bwd_inject(const void* dy, int64_t lddy, const void* x, int64_t
                             int64_t lddx, float* workspace, int rows, int D, float* inj_part, int L, int row0,
                             int nrows, void* stream);
 
+/* Partials-only LayerNorm backward of a tower stored as the first L_live rows of each of its seqs L_full-row
+ * sequences (the EOT-truncated text tower: every later row has exactly zero gradient).  The compact rows are
+ * processed as rows t < L_live of the full tower, so the block partials (workspace: 2 *
+ * mf_layernorm_bwd_blocks(seqs * L_full) * D floats) -- and dgamma / dbeta -- are bit for bit those of
+ * mf_layernorm_bwd over all seqs * L_full rows.  inj_part (optional): the injection backward of
+ * mf_layernorm_bwd_inject (L = L_live).  clip/model.py:153-159 under the causal mask of :679-685.        */
+int mf_layernorm_bwd_live(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* gamma,
+                          const float* mean, const float* rstd, const void* dres, int64_t ldres, void* dx,
+                          int64_t lddx, float* workspace, int seqs, int L_live, int L_full, int D, float* inj_part,
+                          int row0, int nrows, void* stream);
+
 /* dgamma == dbeta == NULL: write the per-block partials only; their reduction is deferred to one
  * mf_col_reduce_batch over all LayerNorms of a backward pass.  desc = {const float* part; float* out;
  * int nblk, C, accumulate, pad} (mf_col_reduce_desc_bytes() bytes each, device memory):
@@ -142,6 +153,10 @@ int mf_seq_grow_bwd(const void* ddst, void* dsrc, int N, int Lp, int ncap, int n
 int mf_caption_pool(const int* tokens, int B, int T, const float* table, int vocab, const void* w, int D,
                     void* pooled, void* stream);
 int mf_transpose_f16(const void* in, int64_t ld_in, void* out, int64_t ld_out, int R, int C, void* stream);
+/* dst row n*L_full + t = src row n*L_live + t (t < L_live; other dst rows untouched), C % 8 == 0 columns: the
+ * EOT-truncated text tower's block-11 weight-gradient operands in the full tower's row layout              */
+int mf_seq_scatter(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, int N, int L_live, int L_full, int C,
+                   void* stream);
 int mf_colsum_blocks(int R);
 /* out[c] = sum_r in[r,c]; workspace: mf_colsum_blocks(R) * C floats                               */
 int mf_colsum_f16(const void* in, int64_t ld, int R, int C, void* out, int out_f16, float* workspace, void* stream);

@@ -291,6 +291,61 @@ def test_layernorm_row_index(dev):
     assert dx[mask].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("D,seqs,L_live,L_full,inject", [(512, 38, 10, 77, False), (512, 38, 10, 77, True),
+                                                         (512, 1000, 13, 77, False), (768, 5, 40, 77, True)])
+def test_layernorm_bwd_live_matches_full_layout(dev, D, seqs, L_live, L_full, inject):
+    """mf_layernorm_bwd_live on the compact first-L_live rows of each sequence == mf_layernorm_bwd(_inject) on
+    the full L_full-row layout whose other rows carry zero dy / dres: same dx rows, bit-identical dgamma / dbeta
+    (and prompt gradient), both below and above the 256-block wide-kernel threshold."""
+    torch.manual_seed(D + seqs)
+    Rf, Rc = seqs * L_full, seqs * L_live
+    live = (torch.arange(Rf, device=dev) % L_full) < L_live
+    xf = (torch.randn(Rf, D, device=dev) * 2 + 0.5).half()
+    g = (1 + 0.1 * torch.randn(D, device=dev))
+    b = 0.1 * torch.randn(D, device=dev)
+    _, mean_f, rstd_f = ops.layernorm_fwd(xf, g, b)
+    dyf = torch.randn(Rf, D, device=dev).half() * live[:, None]
+    dresf = torch.randn(Rf, D, device=dev).half() * live[:, None]
+    xc, dyc, dresc = xf[live].contiguous(), dyf[live].contiguous(), dresf[live].contiguous()
+    mean_c, rstd_c = mean_f[live].contiguous(), rstd_f[live].contiguous()
+    outs = []
+    for full in (True, False):
+        lnb = ops.LNGradBatch(dev)
+        dg = torch.empty(D, device=dev)
+        db = torch.empty(D, device=dev)
+        pg = torch.empty(2, D, device=dev) if inject else None
+        if full:
+            dx = dresf.clone()
+            if inject:
+                lnb.bwd_inject(dyf, xf, g, mean_f, rstd_f, dx, dg, db, dx, pg, L_full, 1, 2)
+            else:
+                lnb.bwd(dyf, xf, g, mean_f, rstd_f, dx, dg, db, dres=dx)
+            dx = dx[live]
+        else:
+            dx = dresc.clone()
+            if inject:
+                lnb.bwd_inject(dyc, xc, g, mean_c, rstd_c, dx, dg, db, dx, pg, L_live, 1, 2, live=(L_live, L_full))
+            else:
+                lnb.bwd(dyc, xc, g, mean_c, rstd_c, dx, dg, db, dres=dx, live=(L_live, L_full))
+        lnb.finish()
+        torch.cuda.synchronize()
+        outs.append((dx, dg, db, pg))
+    (dx0, dg0, db0, pg0), (dx1, dg1, db1, pg1) = outs
+    assert torch.equal(dx0, dx1)
+    assert torch.equal(dg0, dg1) and torch.equal(db0, db1)
+    if inject:
+        assert torch.equal(pg0, pg1)
+
+
+def test_seq_scatter(dev):
+    src = torch.randn(6 * 5, 24, device=dev).half()
+    dst = torch.zeros(6 * 9, 32, device=dev).half()
+    ops.seq_scatter(src, dst[:, :24], 6, 5, 9)
+    ref = torch.zeros(6, 9, 32, device=dev).half()
+    ref[:, :5, :24] = src.view(6, 5, 24)
+    assert torch.equal(dst, ref.view(6 * 9, 32))
+
+
 def _attn_ref(q, k, v, causal):
     """fp64 restatement of the kernel's numerics: P = exp(s - max) rounded to fp16, sum unrounded."""
     s = (q.double() @ k.double().transpose(-1, -2)) * 0.125
