@@ -314,6 +314,68 @@ MF_DEV void lds_bar() {  // s_barrier with LDS ordering and no vmcnt(0): LDS-DMA
   asm volatile("" ::: "memory");
 }
 
+// Forward, persistent over heads: each workgroup (one 16-query tile per wave, ceil(L/16) waves) walks heads
+// blockIdx.x, + gridDim.x, ... with K / V double-buffered in LDS -- the next head's LDS-DMA is issued before the
+// current head's tiles run, so from the second head on the staging hides under the tiles instead of every
+// workgroup life starting with it.  Per tile the arithmetic of attn_fwd4_kernel (fwd4_tile): bit-identical.
+template <int LKP, bool CAUSAL>
+__global__ __launch_bounds__(1024) void attn_fwdp_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
+                                                         f16* __restrict__ out, int64_t ld_out,
+                                                         float* __restrict__ lse, int ld_lse, int L, int H, int NH) {
+  __shared__ __attribute__((aligned(16))) f16 sK[2][LKP * 64];
+  __shared__ __attribute__((aligned(16))) f16 sV[2][LKP * 64];
+  const int D = H * 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4, ii = lane & 15;
+  const int q0 = w * 16;
+  const bool active = q0 < L;
+  int koff[4], voff[8];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int row = 16 * hf + fr;
+      koff[2 * s2 + hf] = row * 64 + (((4 * s2 + fg) ^ (row & 7)) << 3);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) voff[2 * dt + hf] = sw_off(16 * hf + 4 * fg + (ii >> 2), 16 * dt + 4 * (ii & 3));
+  }
+  // this wave's LDS-DMA instructions per head (K and V, stage_rows' row-group split)
+  const int nkv = 2 * (w < LKP / 8 ? (LKP / 8 - w + nw - 1) / nw : 0);
+  int nh = blockIdx.x;
+  if (nh >= NH) return;
+  {
+    const f16* base = qkv + (int64_t)(nh / H) * L * ld_qkv;
+    stage_rows<LKP>(sK[0], base, ld_qkv, L, D + (nh % H) * 64);
+    stage_rows<LKP>(sV[0], base, ld_qkv, L, 2 * D + (nh % H) * 64);
+  }
+  for (int it = 0; nh < NH; ++it, nh += gridDim.x) {
+    const int b = it & 1;
+    const int n = nh / H, h = nh % H;
+    const f16* base = qkv + (int64_t)n * L * ld_qkv;
+    f16x8 qf0, qf1;
+    {
+      const int q = q0 + fr;
+      const f16* qrow = base + (int64_t)(q < L ? q : L - 1) * ld_qkv + h * 64 + 8 * fg;
+      qf0 = *(const f16x8*)qrow;
+      qf1 = *(const f16x8*)(qrow + 32);
+    }
+    const int nn = nh + gridDim.x;
+    int pend = 0;
+    if (nn < NH) {  // the next head into the other buffer (free: the barrier closing the previous iteration)
+      const f16* nb = qkv + (int64_t)(nn / H) * L * ld_qkv;
+      stage_rows<LKP>(sK[b ^ 1], nb, ld_qkv, L, D + (nn % H) * 64);
+      stage_rows<LKP>(sV[b ^ 1], nb, ld_qkv, L, 2 * D + (nn % H) * 64);
+      pend = nkv;
+    }
+    wait_vm_n(pend);  // this head's K / V (issued an iteration earlier) and the Q fragments have landed
+    lds_bar();        // ... for every wave
+    fwd4_tile<LKP, CAUSAL, false>(sK[b], sV[b], koff, voff, qf0, qf1, active, q0, L, lane, out, ld_out, lse, ld_lse,
+                                  (int64_t)n * L, h, nh);
+    lds_bar();  // every wave is done with buffer b before the next iteration stages into it
+  }
+}
+
 // one k-sub of the fused kernel's LDS-DMA: this wave's instructions u (x rows or W rows) into `slot`.  The
 // buffer descriptors are built here from (pointer, byte range): a kernel template whose body holds a
 // descriptor-typed lambda capture or parameter loses its host stub under hipcc (see gemm.hip dma_stage).
@@ -989,6 +1051,35 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
       default: return mf_set_error("attention: bad padded length", -1);
     }
 #undef CALLF4L
+    MF_CHECK_LAUNCH();
+    return 0;
+  }
+  // many heads of a long sequence (the eval engine's 400-image launches: 4 800 heads of 199 rows): the persistent
+  // double-buffered kernel, one workgroup per CU walking ~19 heads (tests/diagnostics/attn_bench.py, r05:
+  // 172.5 -> 148.8 us at 400 images, bit-identical; at 1 200 heads even, at c4's 384 heads 14.1 -> 17.3 us and at
+  // the causal 77-row text heads 79 -> 83 us, so not there)
+  if (N * H >= 2048 && L > 128) {
+    const int tiles = (L + 15) / 16;
+    const int LP16 = tiles * 16;
+    const int per_cu = std::max(1, std::min((160 * 1024) / (512 * LP16), 16 / tiles));
+    const int grid = std::min(N * H, 256 * per_cu);
+#define CALLFP(P)                                                                                                \
+  if (causal)                                                                                                    \
+    attn_fwdp_kernel<P, true><<<grid, 64 * tiles, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H, N * H); \
+  else                                                                                                           \
+    attn_fwdp_kernel<P, false><<<grid, 64 * tiles, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H, N * H);
+    switch (LP16) {
+      case 16: CALLFP(16); break;
+      case 48: CALLFP(48); break;
+      case 80: CALLFP(80); break;
+      case 112: CALLFP(112); break;
+      case 144: CALLFP(144); break;
+      case 176: CALLFP(176); break;
+      case 208: CALLFP(208); break;
+      case 240: CALLFP(240); break;
+      default: MF_ATTN_DISPATCH(LP, CALLFP)
+    }
+#undef CALLFP
     MF_CHECK_LAUNCH();
     return 0;
   }

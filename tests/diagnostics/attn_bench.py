@@ -1,6 +1,7 @@
 """Diagnostic (GPU box): attention fwd/bwd kernel time, TFLOP/s, algorithmic GB/s and roofline
 fraction on the MaPLe shapes (vision N=32 L=199 H=12; text K=38 L=77 H=8 causal; the caption path's
-longer vision sequences, L=263 and 455; the C5 text tower, K=1000 L=77 H=8 causal)."""
+longer vision sequences, L=263 and 455; the C5 text tower, K=1000 L=77 H=8 causal; the eval engine's
+100- and 400-image launches)."""
 import sys
 from pathlib import Path
 
@@ -32,8 +33,11 @@ def timeit(fn, it=20):
 
 
 dev = torch.device("cuda:0")
-for (N, L, H, causal) in [(32, 199, 12, False), (38, 77, 8, True), (4, 199, 12, False), (10, 77, 8, True), (32, 263, 12, False),
-                             (32, 455, 12, False), (1000, 77, 8, True)]:
+SHAPES = [(32, 199, 12, False), (38, 77, 8, True), (4, 199, 12, False), (10, 77, 8, True), (32, 263, 12, False),
+          (32, 455, 12, False), (1000, 77, 8, True), (100, 199, 12, False), (400, 199, 12, False)]
+if len(sys.argv) > 1:  # e.g. "0,7,8": a subset of SHAPES (the eval engine's 100 / 400-image launches are 7, 8)
+    SHAPES = [SHAPES[int(i)] for i in sys.argv[1].split(",")]
+for (N, L, H, causal) in SHAPES:
     D = H * 64
     torch.manual_seed(L + N)
     qkv = torch.randn(N * L, 3 * D, device=dev).half()

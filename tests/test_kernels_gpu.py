@@ -389,6 +389,25 @@ def test_attention_fwd_bwd(dev, N, L, H, causal):
     assert rel < 5e-3, rel
 
 
+@pytest.mark.parametrize("L", [199, 150])
+def test_attention_fwd_many_heads_bit_identical(dev, L):
+    """>= 2 048 heads of > 128 rows run the persistent double-buffered forward (attn_fwdp_kernel): out and lse
+    bit-identical to the per-head kernel run on slices of the batch (batch-invariant rows), and close to fp64."""
+    N, H = 200, 12
+    torch.manual_seed(L)
+    D = H * 64
+    qkv = torch.randn(N * L, 3 * D).half().to(dev)
+    out, lse = ops.attention_fwd(qkv, N, L, H, False)
+    n = 50  # 600 heads per slice: attn_fwd4_kernel
+    for s in range(0, N, n):
+        o_s, l_s = ops.attention_fwd(qkv[s * L:(s + n) * L], n, L, H, False)
+        assert torch.equal(out[s * L:(s + n) * L], o_s)
+        assert torch.equal(lse.view(N * H, -1)[s * H:(s + n) * H, :L], l_s.view(n * H, -1)[:, :L])
+    q, k, v = qkv[:4 * L].view(4, L, 3, H, 64).permute(2, 0, 3, 1, 4).unbind(0)
+    ref = _attn_ref(q, k, v, False).permute(0, 2, 1, 3).reshape(4 * L, D)
+    assert_ulps(out[:4 * L], ref, 4.0, 2e-2, "attn fwd persistent")
+
+
 @pytest.mark.parametrize("N,L,H,causal", [(4, 199, 12, False), (32, 199, 12, False), (3, 193, 12, False),
                                           (38, 77, 8, True), (5, 80, 8, True)])
 def test_qkv_attention_fused_matches_unfused(dev, N, L, H, causal):
