@@ -11,6 +11,6 @@ for s in ${SHAPES:-19900,2304,768 6368,2304,768}; do
     python3 tests/diagnostics/gemm_one.py $M $N $K -2 3 > gpurun_out/blas_names/${M}_${N}_${K}.log 2>&1
   rc=$?; echo "$s rc=$rc"; [ $rc -eq 0 ] || exit $rc
   f=$(ls gpurun_out/blas_names/${M}_${N}_${K}/*kernel_stats.csv 2>/dev/null | head -1)
-  [ -n "$f" ] && python3 -c "import csv,sys; [print('  ', r['Name'][:200], r['AverageNs']) for r in csv.DictReader(open('$f'))]"
+  [ -n "$f" ] && python3 -c "import csv,sys; [print('  ', r['Name'][:600], r['AverageNs']) for r in csv.DictReader(open('$f'))]"
   rm -rf gpurun_out/blas_names/${M}_${N}_${K}
 done
