@@ -382,8 +382,9 @@ def test_caption_generator_shared_by_trainer_and_module(dev, tmp_path):
 
 def test_eot_truncate_config_key(dev, tmp_path):
     """TRAINER.MAPLE.EOT_TRUNCATE (MI355X addition, default off): the client engines run the text tower on
-    the first max(EOT) + 1 tokens, and a training step's logits and loss equal the full 77-token tower's bit
-    for bit (the causal mask makes every later position dead for the EOT features)."""
+    the first max(EOT) + 1 tokens, and a training step's logits, loss and gradients equal the full 77-token
+    tower's bit for bit (the causal mask makes every later position dead for the EOT features; the backward's row
+    reductions run over the 77-row layout)."""
     full = build_trainer(small_cfg(tmp_path / "a", clients=1))
     trunc = build_trainer(small_cfg(tmp_path / "b", clients=1, extra=["TRAINER.MAPLE.EOT_TRUNCATE", True]))
     ef, et = full.clients[0].engine, trunc.clients[0].engine
@@ -394,9 +395,11 @@ def test_eot_truncate_config_key(dev, tmp_path):
         c.engine.clear_halt()
         c._load(batch["img"], batch["label"], c.engine)
         c.engine.forward_backward()
-        out.append((c.engine.logits.detach().cpu().clone(), c.engine.loss()))
+        out.append((c.engine.logits.detach().cpu().clone(), c.engine.loss(),
+                    {k: v.detach().clone() for k, v in c.engine.grads().items()}))
     assert torch.equal(out[0][0], out[1][0])
     assert out[0][1] == out[1][1]
+    assert all(torch.equal(out[0][2][k], out[1][2][k]) for k in out[0][2])
 
 
 def test_eval_group_counts_bit_identical(dev, tmp_path):
