@@ -29,7 +29,7 @@ for name, M, N, K in [("v.dW_fc", 3072, 768, 6368), ("v.dW_proj", 768, 3072, 636
     C = torch.empty(M, N, device=dev, dtype=torch.float16)
     fl = 2.0 * M * N * K
     res = [f"kmajor {fl / timeit(lambda: ops.gemm(dY, X, C, a_kmajor=True, b_kmajor=True)) / 1e6:6.0f}"]
-    for sp in (0, 2, 3, 4, 8):
+    for sp in (0, 1, 2, 3, 4, 6, 8):
         ws = torch.empty(ops.gemm_splitk_ws_floats(M, N, K, sp), device=dev)
         us = timeit(lambda: ops.gemm_splitk(dY, X, C, ws, splits=sp, a_kmajor=True, b_kmajor=True))
         res.append(f"s{sp} {fl / us / 1e6:6.0f} ({us:5.1f}us)")
