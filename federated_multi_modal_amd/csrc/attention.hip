@@ -1062,7 +1062,7 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
     const int tiles = (L + 15) / 16;
     const int LP16 = tiles * 16;
     const int per_cu = std::max(1, std::min((160 * 1024) / (512 * LP16), 16 / tiles));
-    const int grid = std::min(N * H, 256 * per_cu);
+    const int grid = std::min(N * H, mf_cu_count() * per_cu);
 #define CALLFP(P)                                                                                                \
   if (causal)                                                                                                    \
     attn_fwdp_kernel<P, true><<<grid, 64 * tiles, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H, N * H); \

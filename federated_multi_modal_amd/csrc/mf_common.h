@@ -106,3 +106,16 @@ __global__ __launch_bounds__(1024) void col_reduce_kernel(const float* __restric
   } while (0)
 
 extern "C" int mf_set_error(const char* msg, int code);
+
+// Compute units of the current device (256 on an MI355X; fewer under a compute partition mode), cached per device.
+inline int mf_cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cached[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
