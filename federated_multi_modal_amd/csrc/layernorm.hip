@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256) void ln_fwd2_kernel(const f16* __restrict__ x,
 // tower and the small clients), 16 (one row each: twice the waves in flight per row block).  The partials stay bit-identical: a pair of
 // one-row half-waves is summed first (fl(a + b) = fl(b + a), and 0 + a is exact), which is what a two-row
 // half-wave's accumulator holds, then the 8 pair sums in order.
-template <int D, int HWB = 8>
+template <int D, int HWB = 8, bool LIVE = false>
 __global__ __launch_bounds__(HWB * 32) void ln_bwd2_kernel(const f16* __restrict__ dy, int64_t lddy,
                                                      const f16* __restrict__ x, int64_t ldx,
                                                      const int* __restrict__ ridx, const float* __restrict__ gamma,
@@ -288,10 +288,12 @@ __global__ __launch_bounds__(HWB * 32) void ln_bwd2_kernel(const f16* __restrict
                                                      int rows, float* __restrict__ inj_part = nullptr,
                                                      int inj_L = 1, int inj_row0 = 0, int inj_n = 0,
                                                      int seg_live = 0, int seg_full = 0) {
-  // seg_full > 0: `rows` counts VIRTUAL rows of seg_full-row sequences, of which the first seg_live of each are
-  // stored (compact row (v / seg_full) * seg_live + v % seg_full); the rest are rows whose dy is exactly zero
-  // (the text tower's tokens after every class's EOT, mf_layernorm_bwd_live): they are not read and add nothing,
-  // so the row blocks, and with them the dgamma / dbeta partials, are those of the full-length tower
+  // LIVE: `rows` counts VIRTUAL rows of seg_full-row sequences, of which the first seg_live of each are stored
+  // (compact row (v / seg_full) * seg_live + v % seg_full); the rest are rows whose dy is exactly zero (the text
+  // tower's tokens after every class's EOT, mf_layernorm_bwd_live): they add nothing, so the row blocks, and with
+  // them the dgamma / dbeta partials, are those of the full-length tower.  A dead row's loads still run (from
+  // compact row 0, a cache hit) so that the load / wait structure is the plain kernel's: r05 measured a version
+  // that branched around them giving run-to-run different dgamma partials under tower concurrency.
   constexpr int CH = D / 256;
   static_assert(HWB == 8 || HWB == 16, "half-waves per block");
   constexpr int RPH = LN_ROWS_PER_BLOCK / HWB;  // rows per half-wave
@@ -322,13 +324,12 @@ __global__ __launch_bounds__(HWB * 32) void ln_bwd2_kernel(const f16* __restrict
   for (int k = 0; k < RPH; ++k) {
     int row = min(r0 + k, rows - 1);
     use[k] = r0 + k < rows;
-    if (seg_full > 0) {
+    if constexpr (LIVE) {
       const int t = row % seg_full;
       use[k] = use[k] && t < seg_live;
       row = use[k] ? (row / seg_full) * seg_live + t : 0;
     }
     srcs[k] = ridx ? ridx[row] : row;
-    if (seg_full > 0 && !use[k]) continue;  // a zero-gradient row: nothing to read
     means[k] = mean_in[row];
     rstds[k] = rstd_in[row];
 #pragma unroll
@@ -634,7 +635,7 @@ extern "C" int mf_layernorm_bwd_live(const void* dy, int64_t lddy, const void* x
   const int inj_n = inj_part ? nrows : 0;
   hipStream_t st = (hipStream_t)stream;
 #define MF_LN_LIVE(DD, HW, TH)                                                                                       \
-  ln_bwd2_kernel<DD, HW><<<nblk, TH, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, nullptr, gamma, mean, rstd, \
+  ln_bwd2_kernel<DD, HW, true><<<nblk, TH, 0, st>>>((const f16*)dy, lddy, (const f16*)x, ldx, nullptr, gamma, mean, rstd, \
                                               (const f16*)dres, ldres, (f16*)dx, lddx, dg_part, db_part, rows,     \
                                               inj_part, L_live, row0, inj_n, L_live, L_full)
   if (D == 768 && ln_bwd_wide(nblk)) MF_LN_LIVE(768, 16, 512);

@@ -245,6 +245,31 @@ def test_eot_truncated_text_tower_matches_full(dev, J, K, B, seed):
     assert torch.equal(a0, a1) and torch.equal(b0, b1)
 
 
+def test_concurrent_towers_are_reproducible_and_eot_exact(dev):
+    """Three c4-shape engines stepped in lockstep with the towers on two streams (eager steps, client 1's two
+    batches): two EOT-truncated ones and the 77-token one agree bit for bit in every gradient and weight after every
+    step.  r05 regression: a LayerNorm-backward build whose loads sat behind a branch gave run-to-run different
+    dgamma partials only when the towers overlapped (tests/diagnostics/eot_exact_steps.py)."""
+    J, K, B, seed = 9, 38, 32, 0
+    names = syn.synthetic_classnames(K, seed)
+    cb = [syn.client_batch(seed, 1, s, B, K) for s in range(2)]
+    es = [MapleEngine(EngineConfig(batch=B, classnames=names, prompt_depth=J, seed=seed, eot_truncate=t), device=dev)
+          for t in (False, True, True)]
+    for e in es:
+        e.set_lr(0.0026)
+    for s in range(4):
+        for e in es:
+            e.img_in.copy_(torch.from_numpy(cb[s % 2].images).to(dev))
+            e.label_in.copy_(torch.from_numpy(cb[s % 2].labels).to(dev))
+            e.train_step()
+        torch.cuda.synchronize()
+        g = [e.grads() for e in es]
+        for other in (1, 2):
+            bad = [n for n in g[0] if not torch.equal(g[0][n], g[other][n])]
+            assert not bad, f"step {s}, engine {other}: {bad[:4]}"
+            assert torch.equal(es[0].flat16, es[other].flat16) and torch.equal(es[0].flat32, es[other].flat32)
+
+
 def test_tower_order_does_not_change_results(dev):
     """The towers' enqueue order after each fork (EngineConfig.vision_first: vision first by default, text first
     as the A/B baseline) only changes which stream's launches reach the GPU first: every reduction is
