@@ -1,5 +1,5 @@
 """CPU tier: the FedAvg collective protocol (federated_multi_modal_amd/federated.py) and the federated
-round loop (trainers.MaPLeFederated.train) across world_size 2 and 3 gloo ranks, one client per rank,
+round loop (trainers.MaPLeFederated.train) across world_size 2, 3 and 8 gloo ranks, one client per rank,
 checked against the reference's safe_average_weights / check_weights_valid semantics
 (trainers/maple_fed.py:228-325, restated in oracle/maple_oracle.py and pinned to the reference by
 tests/golden/fedavg.npz).
@@ -115,7 +115,9 @@ def _spawn(fn, world, *args):  # noqa: D103
 
 
 @pytest.mark.parametrize("world,bad,mode", [(2, (), "ordered"), (3, (), "ordered"), (3, (1,), "ordered"),
-                                            (2, (0, 1), "ordered"), (3, (), "allreduce"), (2, (1,), "allreduce")])
+                                            (2, (0, 1), "ordered"), (3, (), "allreduce"), (2, (1,), "allreduce"),
+                                            # the federated configs' world size (C4 / C5: 8 clients on 8 ranks)
+                                            (8, (), "ordered"), (8, (5,), "ordered")])
 def test_fedavg_exchange_matches_reference(world, bad, mode):
     res = _spawn(_worker, world, tuple(bad), mode)
     clients = [FakeEngine(r, bad=r in bad) for r in range(world)]
@@ -281,6 +283,7 @@ def _train_worker(rank, world, port, per_rank, fail, late, abort, out):
     (2, 1, {}, {}), (3, 1, {1: (0,)}, {}), (2, 1, {0: (1,), 1: (1,)}, {}),
     (2, 2, {1: (0,)}, {}),                 # 4 clients on 2 ranks, trained two after another per rank
     (2, 1, {}, {1: (1,)}), (2, 2, {}, {0: (0,), 3: (1,)}),  # a client's last test() fails after its bucket went out
+    (8, 1, {3: (0,)}, {6: (1,)}),          # world 8 (C4 / C5: one client per GPU of the node), one bad rank per round
 ])
 def test_round_loop_distributed(world, per_rank, fail, late):
     """MaPLeFederated.train() on gloo ranks: 2 rounds x 2 local epochs; each client's bucket is packed inside
