@@ -411,6 +411,11 @@ class _Tower:
         summation order are the full tower's (its extra rows contribute exact zeros)."""
         if self.live is not None:
             Ll, Lf = self.live
+            # exactness rests on full_dy / full_x rows t >= Ll staying zero: they are zeroed at allocation and the
+            # only writer is this scatter, which writes rows t < Ll of column views that start at the buffers'
+            # own first element (checked here, so no caller can hand it an offset view)
+            for src, full in ((dY, self.full_dy), (Xin, self.full_x)):
+                assert src.shape[0] == self.N * Ll and src.shape[1] <= full.shape[1] and full.shape[0] == self.N * Lf
             dY = ops.seq_scatter(dY, self.full_dy[:, :dY.shape[1]], self.N, Ll, Lf)[:self.N * Lf]
             Xin = ops.seq_scatter(Xin, self.full_x[:, :Xin.shape[1]], self.N, Ll, Lf)[:self.N * Lf]
         if tuple(dW.shape) in self.dw_split:

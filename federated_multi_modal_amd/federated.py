@@ -27,7 +27,9 @@ Two exchange modes (FED.AGGREGATION in the trainer config):
     bit-identical to safe_average_weights at any world size (CPU-torch mean semantics: sum then divide,
     which tests/golden/fedavg.npz pins).  On a GPU the chain runs on a side stream (all_to_all -> reduce
     -> all_gather), so start() returns at once and the caller's next kernels run under it; under gloo (the
-    world-size-2 CPU tests) the same _ordered_chain runs with host waits, so those tests cover its code.
+    world-size 2 / 3 / 8 CPU tests) the same _ordered_chain runs with host waits, so those tests cover its
+    collective order and arithmetic -- not the RCCL stream dependencies, nor the start() / finish() overlap
+    with caller kernels, which only an RCCL run with more than one GPU exercises (the driver's 8-GPU bench).
   * "allreduce": the rank's buckets summed in client order, then one RCCL all_reduce(SUM).  The same
     traffic, but RCCL's ring order changes the fp32 summation order per chunk; with three or more ranks the
     fp16-rounded result can differ from the reference's in the last fp16 bit of rare elements.

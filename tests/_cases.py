@@ -78,6 +78,12 @@ def case_floor(name: str) -> Dict[str, float]:
     return json.loads(path.read_text()).get(name, {}) if path.exists() else {}
 
 
+def fp16_ulp(x: np.ndarray) -> np.ndarray:
+    """The spacing of fp16 values at |x| (subnormal spacing 2^-24 below 2^-14)."""
+    a = np.maximum(np.abs(np.asarray(x, dtype=np.float64)), 2.0 ** -14)
+    return np.exp2(np.floor(np.log2(a)) - 10)
+
+
 def logit_gate(ours: np.ndarray, ref: np.ndarray, ref64: np.ndarray, floor: Dict[str, float] = None):
     """The GPU logit gate.  Two correct fp16 implementations of the model bound it: the
     reference itself and the reference with exactly rounded GEMMs (`floor`, per fixture):
@@ -87,7 +93,10 @@ def logit_gate(ours: np.ndarray, ref: np.ndarray, ref64: np.ndarray, floor: Dict
       * argmax identical on EVERY row (north_star: class predictions bit-exact; r05: all rows, not only those
         whose top-2 margin exceeds the max gate -- the margin-cleared count is still reported);
       * reported beside the gate: the share of logits within north_star's 1e-3 of the reference
-        (`within_1e3`), so the distance to the stated target stays visible next to the floor-relative pass.
+        (`within_1e3`), so the distance to the stated target stays visible next to the floor-relative pass, and
+        the error in fp16 ulps of the reference logit (`max_ulps`, `mean_ulps` over |logit| >= 1/4, `within_1ulp`; r06): the
+        reference's logits are fp16, and wherever |logit| >= 2 one fp16 ulp (2^-9) already exceeds 1e-3
+        (`share_ulp_gt_1e3` = the share of logits where it does).
     Without a floor: 4e-3 / 1.5e-3 and the reference's own fp64 distance.  Returns (ok, report dict)."""
     floor = floor or {}
     ours = ours.astype(np.float64)
@@ -108,6 +117,12 @@ def logit_gate(ours: np.ndarray, ref: np.ndarray, ref64: np.ndarray, floor: Dict
                argmax_all_equal=bool(np.array_equal(ours.argmax(1), ref.argmax(1))),
                argmax_rows_equal=int((ours.argmax(1) == ref.argmax(1)).sum()),
                within_1e3=float((err <= 1e-3).mean()), ref_within_1e3_of64=float((d64_ref <= 1e-3).mean()))
+    ulp = fp16_ulp(ref)
+    big = np.abs(ref) >= 0.25  # ulps of tiny logits are tiny: there the absolute gate speaks (max_ulps over |ref| >= 1/4)
+    ue = err / ulp
+    rep.update(max_ulps=float(ue[big].max()) if big.any() else 0.0, mean_ulps=float(ue[big].mean()) if big.any() else 0.0,
+               within_1ulp=float((err <= ulp).mean()), share_ulp_gt_1e3=float((ulp > 1e-3).mean()),
+               ulp_at_max=float(ulp.flat[int(err.argmax())]))
     ok = (err.max() <= max_gate and err.mean() <= mean_gate and d64_ours.max() <= e64_max_gate
           and d64_ours.mean() <= e64_mean_gate and argmax_ok)
     return ok, rep

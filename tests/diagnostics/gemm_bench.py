@@ -8,6 +8,8 @@ each tile configuration against a torch fp32 matmul.  Prints TFLOP/s.
                                         c5: the K = 1000 text tower's products (77 000 rows)
                                         c3: the B = 4 / K = 10 client's products (796 / 770 rows)
                                         eval: a 100-image test batch's forward products (19 900 rows)
+                                        eval4: the eval engine's launches at EVAL_GROUP 4 (400 images, 79 600
+                                        rows); in both eval sets c_fc stores no pre-activation (forward-only engine)
 
 A "!" marks a tile whose plain product misses the fp32 reference, "~" one whose output (with the
 shape's epilogue) is not bit-identical to the first listed tile's.
@@ -79,9 +81,10 @@ def main():
                   ("c3t.fc", 770, 2048, 512, ops.EPI_BIAS_GELU, 12), ("c3t.proj", 770, 512, 2048, ops.EPI_BIAS_RESID, 12),
                   ("c3t.dfc", 770, 2048, 512, ops.EPI_DGELU, 12), ("c3t.dh", 770, 512, 2048, ops.EPI_NONE, 12),
                   ("c3t.do", 770, 512, 512, ops.EPI_NONE, 12), ("c3t.dqkv", 770, 512, 1536, ops.EPI_NONE, 12)]
-    if len(sys.argv) > 2 and sys.argv[2] == "eval":  # test() batches: 100 images (19 900 rows), forward only
-        shapes = [("ev.qkv", 19900, 2304, 768, ops.EPI_BIAS, 12), ("ev.out", 19900, 768, 768, ops.EPI_BIAS_RESID, 12),
-                  ("ev.fc", 19900, 3072, 768, ops.EPI_BIAS_GELU, 12), ("ev.proj", 19900, 768, 3072, ops.EPI_BIAS_RESID, 12)]
+    evalm = {"eval": 19900, "eval4": 79600}.get(sys.argv[2] if len(sys.argv) > 2 else "")
+    if evalm:  # test() batches: 100 (or 4 x 100) images, forward only
+        shapes = [("ev.qkv", evalm, 2304, 768, ops.EPI_BIAS, 12), ("ev.out", evalm, 768, 768, ops.EPI_BIAS_RESID, 12),
+                  ("ev.fc", evalm, 3072, 768, ops.EPI_BIAS_GELU, 12), ("ev.proj", evalm, 768, 3072, ops.EPI_BIAS_RESID, 12)]
     if len(sys.argv) > 2 and sys.argv[2] == "big":
         shapes = [("4096^3", 4096, 4096, 4096, ops.EPI_NONE, 1), ("8192^3", 8192, 8192, 8192, ops.EPI_NONE, 1),
                   ("v.fc K4k", 6368, 3072, 4096, ops.EPI_NONE, 1), ("v.qkv K3k", 6368, 2304, 3072, ops.EPI_NONE, 1)]
@@ -104,7 +107,7 @@ def main():
                 kw["bias"] = bias
             if epi in (ops.EPI_BIAS_RESID, ops.EPI_DGELU):
                 kw["aux_in"] = aux
-            if epi == ops.EPI_BIAS_GELU:
+            if epi == ops.EPI_BIAS_GELU and not evalm:
                 kw["aux_out"] = auxo
             try:
                 ops.gemm_nt(A, B, **kw)

@@ -1,4 +1,10 @@
-"""Static check of the vector-memory wait counts in gfx950 kernel assembly (test tooling, not product).
+"""ISA tooling for the CPU tier (test tooling, not product): the gfx950 code objects inside libmapfed.so, their
+disassembly, and a static check of the vector-memory wait counts.
+
+``device_disassembly(so_path)`` unbundles the ``.hip_fatbin`` section (clang offload bundles, one per translation
+unit) and returns ``llvm-objdump -d`` of every gfx950 code object, split by kernel symbol.
+
+Wait counts:
 
 Every VGPR a global / buffer load writes is "in flight" until an ``s_waitcnt vmcnt(N)`` retires it: the
 hardware decrements vmcnt in issue order for loads and stores alike (gfx9 has no separate store counter),
@@ -14,7 +20,57 @@ latency.
 from __future__ import annotations
 
 import re
+import struct
+import subprocess
+import tempfile
 from dataclasses import dataclass, field
+from pathlib import Path
+
+LLVM_BIN = Path("/opt/rocm/lib/llvm/bin")
+_BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def code_objects(so_path) -> list[bytes]:
+    """The gfx950 code objects (ELF images) of a HIP shared library's .hip_fatbin section."""
+    with tempfile.TemporaryDirectory() as td:
+        fat = Path(td) / "fat.bin"
+        subprocess.run([str(LLVM_BIN / "llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}", str(so_path),
+                        str(Path(td) / "discard")], check=True, capture_output=True)
+        data = fat.read_bytes()
+    out, i = [], 0
+    while True:
+        i = data.find(_BUNDLE_MAGIC, i)
+        if i < 0:
+            return out
+        (n,) = struct.unpack_from("<Q", data, i + 24)
+        p = i + 32
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", data, p)
+            triple = data[p + 24:p + 24 + tlen].decode()
+            p += 24 + tlen
+            if "gfx950" in triple and size:
+                out.append(data[i + off:i + off + size])
+        i += len(_BUNDLE_MAGIC)
+
+
+def device_disassembly(so_path) -> dict[str, list[str]]:
+    """kernel symbol -> its disassembled instruction lines, over every gfx950 code object of the library."""
+    kernels: dict[str, list[str]] = {}
+    with tempfile.TemporaryDirectory() as td:
+        for n, co in enumerate(code_objects(so_path)):
+            f = Path(td) / f"co{n}.elf"
+            f.write_bytes(co)
+            txt = subprocess.run([str(LLVM_BIN / "llvm-objdump"), "-d", "--no-show-raw-insn", str(f)], check=True,
+                                 capture_output=True, text=True).stdout
+            cur = None
+            for ln in txt.splitlines():
+                m = re.match(r"^[0-9a-f]+ <(\S+)>:$", ln)
+                if m:
+                    cur = m.group(1)
+                    kernels[cur] = []
+                elif cur is not None and ln.strip():
+                    kernels[cur].append(ln.strip())
+    return kernels
 
 _VREG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
 _WAIT = re.compile(r"vmcnt\((\d+)\)")

@@ -213,6 +213,29 @@ def test_eval_reuses_text_features_bit_exactly(dev):
     assert acc[1].item() == B
 
 
+def test_eval_launch_size_does_not_change_logits(dev):
+    """The precondition of TRAINER.MAPLE.EVAL_GROUP > 1 at the reference's cadence (PatternNet, TEST.BATCH_SIZE 100):
+    one 400-image forward of the forward-only eval engine -- other GEMM tiles, and at 4 800 heads the persistent
+    attention forward -- gives the rows of four 100-image forwards (1 200 heads: attn_fwd4) bit for bit, so the
+    accuracy counts of a grouped test pass are those of batch-by-batch evaluation (trainers/maple.py:660-681)."""
+    J, K, seed = 9, 38, 3
+    names = syn.synthetic_classnames(K, seed)
+    big = MapleEngine(EngineConfig(batch=400, classnames=names, prompt_depth=J, seed=seed, inference=True),
+                      device=dev)
+    small = MapleEngine(EngineConfig(batch=100, classnames=names, prompt_depth=J, seed=seed, inference=True),
+                        device=dev, shared=big)
+    imgs = torch.cat([torch.from_numpy(syn.client_batch(seed, 0, s, 100, K).images) for s in range(4)])
+    big.load_batch(imgs)
+    lb = big.forward().clone()
+    rows = []
+    for s in range(4):
+        small.load_batch(imgs[100 * s:100 * (s + 1)])
+        rows.append(small.forward().clone())
+    ls = torch.cat(rows)
+    assert torch.isfinite(lb.float()).all()
+    assert torch.equal(lb, ls), (lb.float() - ls.float()).abs().max().item()
+
+
 @pytest.mark.parametrize("J,K,B,seed", [(3, 10, 4, 4), (9, 38, 8, 1)])
 def test_eot_truncated_text_tower_matches_full(dev, J, K, B, seed):
     """EngineConfig.eot_truncate: the text tower on the first max(EOT)+1 tokens of each class prompt.  Under the
