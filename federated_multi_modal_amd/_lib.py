@@ -24,6 +24,7 @@ SIGNATURES = {
     "mf_col_reduce_desc_bytes": [],
     "mf_col_reduce_batch": [P, I, I, P],
     "mf_attention_fwd": [P, L, P, L, P, I, I, I, I, I, P],
+    "mf_attention_fwd_rows": [P, L, P, L, P, I, I, I, I, I, I, P],
     "mf_attention_bwd": [P, L, P, L, P, L, P, P, I, P, L, I, I, I, I, P],
     "mf_qkv_attention_fwd": [P, L, I, P, P, P, L, P, L, P, I, I, I, I, I, P],
     "mf_qkv_attention_supported": [I, I, I, I],

@@ -228,7 +228,10 @@ MF_DEV void fwd4_tile(const f16* sK, const f16* sV, const int* koff, const int* 
 template <int LKP, bool CAUSAL, int MAXT = 1024>
 __global__ __launch_bounds__(MAXT) void attn_fwd4_kernel(const f16* __restrict__ qkv, int64_t ld_qkv,
                                                            f16* __restrict__ out, int64_t ld_out,
-                                                           float* __restrict__ lse, int ld_lse, int L, int H) {
+                                                           float* __restrict__ lse, int ld_lse, int L, int H,
+                                                           int Lq) {
+  // Lq <= L: only query rows 0 .. Lq-1 of each head are computed (their tiles; a tile's rows past Lq still are,
+  // bit for bit as in a full launch: every query's arithmetic is independent of the other tiles)
   __shared__ __attribute__((aligned(16))) f16 sK[LKP * 64];
   __shared__ __attribute__((aligned(16))) f16 sV[LKP * 64];
   const int D = H * 64;
@@ -238,7 +241,7 @@ __global__ __launch_bounds__(MAXT) void attn_fwd4_kernel(const f16* __restrict__
   const int fr = lane & 15, fg = lane >> 4, ii = lane & 15;
   const int qstep = gridDim.y * nw * 16;
   int q0 = (blockIdx.y * nw + w) * 16;
-  const bool active = q0 < L;
+  const bool active = q0 < Lq;
   MF_ASTAMP2(0);
   f16x8 qf0, qf1;
   {
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(MAXT) void attn_fwd4_kernel(const f16* __restrict__
   fwd4_tile<LKP, CAUSAL, true>(sK, sV, koff, voff, qf0, qf1, active, q0, L, lane, out, ld_out, lse, ld_lse,
                                (int64_t)n * L, h, nh);
   MF_ASTAMP2(2);
-  for (q0 += qstep; q0 < L; q0 += qstep) {
+  for (q0 += qstep; q0 < Lq; q0 += qstep) {
     const int q = q0 + fr;
     const f16* qrow = base + (int64_t)(q < L ? q : L - 1) * ld_qkv + h * 64 + 8 * fg;
     qf0 = *(const f16x8*)qrow;
@@ -1030,7 +1033,7 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
     const int qs4 = attn_qsplit(N * H, L), tiles = (L + 15) / 16;
     const dim3 grid4(N * H, qs4), block4(64 * std::min(8, (tiles + qs4 - 1) / qs4));
 #define CALLF4L(P) \
-  attn_fwd4_kernel<P, false, 512><<<grid4, block4, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); break;
+  attn_fwd4_kernel<P, false, 512><<<grid4, block4, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H, L); break;
     switch (tiles * 16) {
       case 272: CALLF4L(272)
       case 288: CALLF4L(288)
@@ -1085,15 +1088,16 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
   }
   {
     // the head's 16-query tiles split evenly over its workgroups (no workgroup without a tile)
+    const int Lq = L;
     const int qs4 = attn_qsplit(N * H, L), tiles = (L + 15) / 16;
     const int nw4 = std::min(16, (tiles + qs4 - 1) / qs4);
     const dim3 grid4(N * H, qs4), block4(64 * nw4);
     const int LP16 = tiles * 16;  // keys staged in 16-row tiles (LP16 % 32 == 16: a half last chunk)
 #define CALLF4(P)                                                                                             \
   if (causal)                                                                                                 \
-    attn_fwd4_kernel<P, true><<<grid4, block4, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H); \
+    attn_fwd4_kernel<P, true><<<grid4, block4, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H, Lq); \
   else                                                                                                        \
-    attn_fwd4_kernel<P, false><<<grid4, block4, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H);
+    attn_fwd4_kernel<P, false><<<grid4, block4, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H, Lq);
     switch (LP16) {
       case 16: CALLF4(16); break;
       case 48: CALLF4(48); break;
@@ -1109,6 +1113,42 @@ extern "C" int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int6
     MF_CHECK_LAUNCH();
     return 0;
   }
+}
+
+// The first q_rows query rows of every head only (K / V of all L rows): the forward-only engine's last vision block,
+// whose output is read only at each image's class token (ln_post, clip/model.py:567), needs query row 0 of every
+// head.  One workgroup per head, one wave per 16-query tile; each computed row is bit-identical to mf_attention_fwd's.
+extern "C" int mf_attention_fwd_rows(const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* lse,
+                                     int ld_lse, int N, int L, int H, int causal, int q_rows, void* stream) {
+  if (N <= 0) return 0;
+  if (L <= 0 || L > 256) return mf_set_error("mf_attention_fwd_rows: 0 < L <= 256 required", -1);
+  if (q_rows <= 0 || q_rows > L) return mf_set_error("mf_attention_fwd_rows: 0 < q_rows <= L required", -1);
+  if (ld_lse < L || (ld_qkv % 8) || (ld_out % 4)) return mf_set_error("mf_attention_fwd_rows: bad strides", -1);
+  const int LP = padded_len(L);
+  hipStream_t st = (hipStream_t)stream;
+  const int Lq = q_rows;
+  const int tiles = (L + 15) / 16;
+  const dim3 grid4(N * H, 1), block4(64 * ((q_rows + 15) / 16));
+  const int LP16 = tiles * 16;
+#define CALLF4(P)                                                                                             \
+  if (causal)                                                                                                 \
+    attn_fwd4_kernel<P, true><<<grid4, block4, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H, Lq); \
+  else                                                                                                        \
+    attn_fwd4_kernel<P, false><<<grid4, block4, 0, st>>>((const f16*)qkv, ld_qkv, (f16*)out, ld_out, lse, ld_lse, L, H, Lq);
+  switch (LP16) {
+    case 16: CALLF4(16); break;
+    case 48: CALLF4(48); break;
+    case 80: CALLF4(80); break;
+    case 112: CALLF4(112); break;
+    case 144: CALLF4(144); break;
+    case 176: CALLF4(176); break;
+    case 208: CALLF4(208); break;
+    case 240: CALLF4(240); break;
+    default: MF_ATTN_DISPATCH(LP, CALLF4)
+  }
+#undef CALLF4
+  MF_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int mf_attention_bwd(const void* qkv, int64_t ld_qkv, const void* out, int64_t ld_out, const void* dout,

@@ -276,6 +276,11 @@ class _Tower:
         self.R = R
         e = lambda *s, dt=F16: torch.empty(*s, device=dev, dtype=dt)
         self.inference = bool(eng.cfg.inference)
+        # cls_only (set by MapleEngine for a forward-only vision tower): the last block computes only what row 0 of
+        # each sequence of its output needs (the class token that ln_post reads, clip/model.py:567) -- K / V of every
+        # row, query 0's attention, and out-proj / ln_2 / MLP on the N class rows; each row's arithmetic is the full
+        # block's (GEMM rows and attention queries are independent), so the class rows are bit-identical
+        self.cls_only = False
         if self.inference:
             if any(self.grow):
                 raise NotImplementedError("EngineConfig.inference with growing (caption) sequences")
@@ -382,6 +387,9 @@ class _Tower:
             else:
                 ops.layernorm_fwd(x, self.p(i, "ln_1.weight"), self.p(i, "ln_1.bias"), h1, self.mean1[i],
                                   self.rstd1[i])
+            if self.cls_only and i == self.layers - 1:
+                self._last_block_cls_rows(i, x, h1, L)
+                continue
             if self.fused_qkv_attn and ops.qkv_attention_supported(N, L, H, self.causal):
                 # in-projection + attention in one launch (bit-identical to the pair below)
                 ops.qkv_attention_fwd(h1, self.p(i, "attn.in_proj_weight"), self.p(i, "attn.in_proj_bias"),
@@ -404,6 +412,26 @@ class _Tower:
             if i + 1 < self.layers and self.grow[i + 1]:
                 ops.seq_grow(self.Y[i], self.X[i + 1], cap, deep_prompts[i], N, L, self.ncap, N_CTX, D)
         # self.H1 / H2 / G now hold the last layer's (block 11) tensors, kept for its dW
+
+    def _last_block_cls_rows(self, i: int, x: torch.Tensor, h1: torch.Tensor, L: int):
+        """Block i (the last) of a forward-only tower for the rows n * L only (cls_only): the in-projection of every
+        row (keys and values), the attention of query row 0 (mf_attention_fwd_rows), then out-proj + residual, ln_2
+        and the MLP on the N class rows through strided views (row n * L of O, X1, Y)."""
+        N, H = self.N, self.H
+        ops.gemm_nt(h1, self.p(i, "attn.in_proj_weight"), self.QKV[i], bias=self.p(i, "attn.in_proj_bias"),
+                    epilogue=ops.EPI_BIAS, tile=self.tile)
+        ops.attention_fwd_rows(self.QKV[i], N, L, H, self.causal, 1, out=self.O[i], lse=self.LSE[i])
+        x1 = self.X1[i][::L]
+        ops.gemm_nt(self.O[i][::L], self.p(i, "attn.out_proj.weight"), x1, bias=self.p(i, "attn.out_proj.bias"),
+                    aux_in=x[::L], epilogue=ops.EPI_BIAS_RESID, tile=self.tile)
+        h2 = self.H2[:N]
+        ops.layernorm_fwd(x1, self.p(i, "ln_2.weight"), self.p(i, "ln_2.bias"), h2, self.mean2[i][:N],
+                          self.rstd2[i][:N])
+        g = self.G[:N]
+        ops.gemm_nt(h2, self.p(i, "mlp.c_fc.weight"), g, bias=self.p(i, "mlp.c_fc.bias"), epilogue=ops.EPI_BIAS_GELU,
+                    tile=self.tile)
+        ops.gemm_nt(g, self.p(i, "mlp.c_proj.weight"), self.Y[i][::L], bias=self.p(i, "mlp.c_proj.bias"), aux_in=x1,
+                    epilogue=ops.EPI_BIAS_RESID, tile=self.tile)
 
     def _dw(self, dY: torch.Tensor, Xin: torch.Tensor, dW: torch.Tensor, db: torch.Tensor):
         """dW[out,in] = dY^T . Xin (fp16 out; both operands read K-major in place, K = rows), db = colsum(dY).
@@ -539,6 +567,8 @@ class MapleEngine:
             # C5; r04 same-box A/Bs)
             for t in (self.vis, self.txt):
                 t.fused_qkv_attn = t.tile == -1 and t.Rs[0] >= 2048
+        # a forward-only engine's vision tower: ln_post reads the last block's output at the class rows only
+        self.vis.cls_only = bool(cfg.inference) and not cfg.captions
         self.side = torch.cuda.Stream(device=self.device)
         self.overlap_towers = True  # False: both towers on the current stream (isolated kernel timing)
         self.vision_first = cfg.vision_first  # tower enqueue order after each fork (EngineConfig)

@@ -378,6 +378,23 @@ def attention_fwd(qkv, N, L, H, causal, out=None, lse=None, ld_lse=None):
     return out, lse
 
 
+def attention_fwd_rows(qkv, N, L, H, causal, q_rows, out, lse, ld_lse=None):
+    """attention_fwd for query rows 0 .. q_rows-1 of every head only (their 16-row tiles are computed and stored;
+    each row bit-identical to attention_fwd's): out / lse rows of the other queries are left untouched."""
+    if ld_lse is None:
+        ld_lse = L
+    ev = None
+    if _PROBE is not None and _PROBE.wants("attention"):
+        rows = min(L, (q_rows + 15) // 16 * 16)
+        ev = _PROBE.around(4.0 * N * H * rows * L * 64, N * H * (2.0 * 2 * 64 * L + 2.0 * 2 * 64 * rows),
+                           f"attention_fwd_rows/L{L}")
+    call("mf_attention_fwd_rows", _p(qkv), _ld(qkv), _p(out), _ld(out), _p(lse), ld_lse, N, L, H, int(causal), q_rows,
+         _s())
+    if ev is not None:
+        ev.record()
+    return out, lse
+
+
 def qkv_attention_supported(N, L, H, causal) -> bool:
     return bool(call("mf_qkv_attention_supported", N, L, H, int(causal)))
 

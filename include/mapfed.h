@@ -112,6 +112,11 @@ int mf_col_reduce_batch(const void* descs, int n, int max_cols, void* stream);
  * — qkv [N*L, 3*H*64], out [N*L, H*64], lse [N*H, ld_lse]                                         */
 int mf_attention_fwd(const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* lse, int ld_lse, int N,
                      int L, int H, int causal, void* stream);
+/* The first q_rows query rows of every head only (K / V of all L <= 256 rows; each computed row bit-identical to
+ * mf_attention_fwd's): the forward-only engine's last vision block, whose output ln_post reads only at the class
+ * token (clip/model.py:567), attends query row 0 (r06).                                              */
+int mf_attention_fwd_rows(const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* lse, int ld_lse, int N,
+                          int L, int H, int causal, int q_rows, void* stream);
 /* The in-projection and the attention forward in one launch: qkv = fp16(x w^T + bias) (w = in_proj_weight
  * [3D, D], bias [3D]; bit-identical to mf_gemm_nt's EPI_BIAS) is written to qkv [N*L, 3D] and attended
  * as mf_attention_fwd does (bit-identical out / lse).  Shapes: the vision blocks (D = 768, 193..208

@@ -234,6 +234,12 @@ def test_eval_launch_size_does_not_change_logits(dev):
     ls = torch.cat(rows)
     assert torch.isfinite(lb.float()).all()
     assert torch.equal(lb, ls), (lb.float() - ls.float()).abs().max().item()
+    # the forward-only engine computes its last vision block for the class rows only (cls_only, r06): the full
+    # block gives the same logits bit for bit
+    assert big.vis.cls_only and small.vis.cls_only
+    big.vis.cls_only = False
+    big.load_batch(imgs)
+    assert torch.equal(big.forward(), lb)
 
 
 @pytest.mark.parametrize("J,K,B,seed", [(3, 10, 4, 4), (9, 38, 8, 1)])

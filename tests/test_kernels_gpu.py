@@ -408,6 +408,26 @@ def test_attention_fwd_many_heads_bit_identical(dev, L):
     assert_ulps(out[:4 * L], ref, 4.0, 2e-2, "attn fwd persistent")
 
 
+@pytest.mark.parametrize("N,L,H,causal,q_rows", [(400, 199, 12, False, 1), (32, 199, 12, False, 1),
+                                                 (3, 199, 12, False, 40), (38, 77, 8, True, 1), (5, 80, 8, True, 17)])
+def test_attention_fwd_rows_bit_identical(dev, N, L, H, causal, q_rows):
+    """mf_attention_fwd_rows (query rows 0 .. q_rows-1 of every head: the forward-only engine's last vision block)
+    against the full forward (attn_fwd4 or, at >= 2 048 heads, the persistent attn_fwdp): every computed query
+    tile's out and lse rows bit-identical, the other rows untouched."""
+    D = H * 64
+    torch.manual_seed(q_rows + L)
+    qkv = torch.randn(N * L, 3 * D).half().to(dev)
+    out, lse = ops.attention_fwd(qkv, N, L, H, causal)
+    o2 = torch.full_like(out, 7.0)
+    l2 = torch.full_like(lse, 7.0)
+    ops.attention_fwd_rows(qkv, N, L, H, causal, q_rows, o2, l2)
+    rows = min(L, (q_rows + 15) // 16 * 16)
+    o_v, o2_v = out.view(N, L, D), o2.view(N, L, D)
+    assert torch.equal(o_v[:, :rows], o2_v[:, :rows])
+    assert (o2_v[:, rows:] == 7.0).all()
+    assert torch.equal(lse.view(N * H, L)[:, :rows], l2.view(N * H, L)[:, :rows])
+
+
 @pytest.mark.parametrize("N,L,H,causal", [(4, 199, 12, False), (32, 199, 12, False), (3, 193, 12, False),
                                           (38, 77, 8, True), (5, 80, 8, True)])
 def test_qkv_attention_fused_matches_unfused(dev, N, L, H, causal):
