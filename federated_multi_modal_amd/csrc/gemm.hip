@@ -1158,8 +1158,9 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
       // shape, so the tile's own efficiency decides (gemm_bench.py ... c5): the full-line 256x256 kernel for
       // N >= 1536 or K >= 1024 (r05, profiles/r05_v1_gemm8f_c5.txt: c5.dh 878 -> 946, c5.dqkv 832 -> 905, c5.proj
       // 827 -> 875, c5.fc 591 -> 612 TFLOP/s), 160x128 for the N = 512, K = 512 products (c5.out 623 / 581, c5.do
-      // 735 / 663 on 160x128 / 256x256)
-      tile = (N >= 1536 || K >= 1024) ? 40 : 10;
+      // 735 / 663 on 160x128 / 256x256); r06: the eval engine's out-projection (M = 79 600 at EVAL_GROUP 4, N = K =
+      // 768) 711..741 on 256x256 against 692..700 on 160x128 (profiles/r06_v1_gemm_eval4_*.txt, r06_v2_*)
+      tile = (N >= 1536 || K >= 1024 || (N >= 768 && K >= 768)) ? 40 : 10;
     else if (M >= 4096 && K >= 512)  // vision products (M = 6368), tests/diagnostics/gemm_bench.py:
       // N = 3072: 160x128 (960 tiles); N = 768: 96x128 (402 tiles, two workgroups per CU) for K >= 2048,
       // 160x64 (480 tiles) for K = 768; +6..37 % over the 128-row tiles
