@@ -414,12 +414,14 @@ class _Tower:
         # self.H1 / H2 / G now hold the last layer's (block 11) tensors, kept for its dW
 
     def _last_block_cls_rows(self, i: int, x: torch.Tensor, h1: torch.Tensor, L: int):
-        """Block i (the last) of a forward-only tower for the rows n * L only (cls_only): the in-projection of every
-        row (keys and values), the attention of query row 0 (mf_attention_fwd_rows), then out-proj + residual, ln_2
-        and the MLP on the N class rows through strided views (row n * L of O, X1, Y)."""
-        N, H = self.N, self.H
-        ops.gemm_nt(h1, self.p(i, "attn.in_proj_weight"), self.QKV[i], bias=self.p(i, "attn.in_proj_bias"),
-                    epilogue=ops.EPI_BIAS, tile=self.tile)
+        """Block i (the last) of a forward-only tower for the rows n * L only (cls_only): the key / value part of the
+        in-projection for every row and its query part for the class rows, the attention of query row 0
+        (mf_attention_fwd_rows; the other queries of its 16-row tile read stale q rows and are not used), then
+        out-proj + residual, ln_2 and the MLP on the N class rows through strided views (row n * L of O, X1, Y)."""
+        N, H, D = self.N, self.H, self.D
+        w, b = self.p(i, "attn.in_proj_weight"), self.p(i, "attn.in_proj_bias")
+        ops.gemm_nt(h1, w[D:], self.QKV[i][:, D:], bias=b[D:], epilogue=ops.EPI_BIAS, tile=self.tile)
+        ops.gemm_nt(h1[::L], w[:D], self.QKV[i][::L, :D], bias=b[:D], epilogue=ops.EPI_BIAS, tile=self.tile)
         ops.attention_fwd_rows(self.QKV[i], N, L, H, self.causal, 1, out=self.O[i], lse=self.LSE[i])
         x1 = self.X1[i][::L]
         ops.gemm_nt(self.O[i][::L], self.p(i, "attn.out_proj.weight"), x1, bias=self.p(i, "attn.out_proj.bias"),
