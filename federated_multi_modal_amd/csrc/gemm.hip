@@ -977,6 +977,270 @@ __global__ __launch_bounds__(512) void gemm8f_kernel(GemmArgs g) {
   MF_STAMP(3);
 }
 
+// gemm8p: gemm8f made persistent for launches of many rounds of 256x256 tiles (the eval engine's products at
+// EVAL_GROUP 4, M = 79 600; the C5 text tower, M = 77 000).  In-kernel stamps of gemm8f on those launches
+// (tests/diagnostics/gemm_stamps.cpp, profiles/r06_v6_gemm_stamps_eval4.txt): a 12-K-step tile lives ~29 us, of
+// which the prologue (the first K-tile's DMA round trip) is ~4 us and the epilogue ~4-7 us, and a new workgroup
+// starts ~3 us after its predecessor ends -- with one 160 KB workgroup per CU nothing else runs meanwhile.  Here one
+// workgroup per CU walks its XCD's tiles (the positions tile_of gives the XCD), and where the epilogue reads no
+// global operand (EPI_NONE / EPI_BIAS / EPI_BIAS_GELU) the NEXT tile's first six half-tiles are issued into the
+// (by then free) ring before this tile's epilogue, whose results go straight from registers to buffer stores (no
+// LDS staging; rows past M fall outside the buffer range and are dropped, so every wave issues the same count and
+// the counted vmcnt stays exact).  Epilogues that read aux (residual, QuickGELU') run before the next prologue:
+// a plain load while LDS-DMA is in flight would make the compiler drain it.  Main loop, fragment reads, MFMA
+// order and the epilogue arithmetic are gemm8f's / epilogue_store's: bit-identical (tests/test_kernels_gpu.py).
+// Needs N % 256 == 0, K % 64 == 0, fp16 C, 16-byte aligned C / aux with 8-element strides (the host checks).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// s_waitcnt lgkmcnt(0) alone (vmcnt 63 = no wait): this wave's ds_reads / ds_writes done, LDS-DMA left in flight
+MF_DEV void wait_lgkm0() { __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14)); }
+
+// gemm8p's epilogue while the next tile's first six half-tiles fly into ring slots 0..5: the tile's two 128-row
+// halves in turn staged through slots 6..9 ([128][256] fp16, 16-byte chunk c of row r at c ^ (r & 7)) by the four
+// waves that own the half, then every thread streams 16-byte chunks out (full cache lines) through buffer stores
+// (rows past M fall outside the range: dropped, so each thread issues exactly 8 stores per half, 8 more for the
+// pre-activation).  The arithmetic is epilogue_store's: fp16(acc + bias), then epi8's QuickGELU.
+template <int EPI>
+MF_DEV void epilogue_staged8p(const GemmArgs& g, f16* stage, const f32x4 (&acc)[8][4], const f16x4 (&bv)[4], int m0,
+                              int n0, int wm, int wn, int tid, int fr, int fg, __amdgpu_buffer_rsrc_t c_rsrc,
+                              __amdgpu_buffer_rsrc_t x_rsrc) {
+  static_assert(EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_BIAS_GELU, "epilogues without a global read");
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    if (wm == hh) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = i * 16 + fr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = wn * 64 + j * 16 + 4 * fg;
+          f16x4 t;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) t[e] = (f16)(acc[i][j][e] + (float)bv[j][e]);
+            else t[e] = (f16)acc[i][j][e];
+          }
+          *(f16x4*)(stage + r * 256 + ((((col >> 3) ^ (r & 7))) << 3) + (col & 7)) = t;
+        }
+      }
+    }
+    wait_lgkm0();
+    lds_barrier();
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+      const int r = pass * 16 + (tid >> 5), c = tid & 31;
+      const f16x8 tv = *(const f16x8*)(stage + r * 256 + ((c ^ (r & 7)) << 3));
+      const int m = m0 + hh * 128 + r, n = n0 + 8 * c;
+      f16x8 out;
+      if constexpr (EPI == EPI_NONE || EPI == EPI_BIAS) {
+        out = tv;
+      } else {
+        if (g.aux_out)  // the pre-activation, non-temporal (st16_stream's policy)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tv), x_rsrc,
+                                                 (int)(((int64_t)m * g.ld_aux + n) * 2), 0, 2);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float t2;
+          out[e] = (f16)quick_gelu16((float)tv[e], &t2);
+        }
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, out), c_rsrc,
+                                             (int)(((int64_t)m * g.ldc + n) * 2), 0, 0);
+    }
+    wait_lgkm0();
+    lds_barrier();  // the staging area is read before the next half (or the next tile's DMA) overwrites it
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
+  constexpr int BM = 256, BN = 256, WN = 4;
+  constexpr int WTM = 128, WTN = 64, QTM = 4, TN = 4, TM = 8;
+  constexpr int HALF = 128 * BK;
+  constexpr int NSLOT = 10, E = 6;
+  static_assert(!epi_reads_aux<EPI>(), "epilogues that read a global operand stay on gemm8f");
+  static_assert(NSLOT * HALF * 2 <= 160 * 1024 && BM * (BN + 8) <= NSLOT * HALF && 128 * 256 <= 4 * HALF, "LDS");
+  __shared__ __attribute__((aligned(1024))) f16 lds[NSLOT * HALF];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_m = (g.M + BM - 1) / BM, tiles_n = g.N / BN;
+  const int T = tiles_m * tiles_n;
+  // this workgroup's positions: XCD x's contiguous range (the bijective remap of the one-shot kernels), every
+  // nl-th position from l
+  const int x = blockIdx.x & 7, l = blockIdx.x >> 3, nl = gridDim.x >> 3;
+  const int q8 = T >> 3, r8 = T & 7;
+  const int pstart = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
+  const int psize = q8 + (x < r8 ? 1 : 0);
+  int k = l;
+  if (k >= psize) return;  // whole workgroup
+
+  const int lrow = lane >> 3, schunk = (lane & 7) ^ lrow;
+  const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.A, 0, (int)(((int64_t)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t b_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.B, 0, (int)(((int64_t)(g.N - 1) * g.ldb + g.K) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t c_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      g.C, 0, (int)(((int64_t)(g.M - 1) * g.ldc + g.N) * 2), 0x00020000);
+  const void* xptr = (const void*)g.aux_out;
+  const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)xptr, 0, xptr ? (int)(((int64_t)(g.M - 1) * g.ld_aux + g.N) * 2) : 0, 0x00020000);
+  const int a_voff = (lrow * (int)g.lda + schunk * 8) * 2;
+  const int b_voff = (lrow * (int)g.ldb + schunk * 8) * 2;
+  auto slot = [&](int h) { return lds + (h % NSLOT) * HALF; };
+  int m0, n0;
+  auto tile_at = [&](int kk, int& mm0, int& nn0) {
+    int mt, nt;
+    tile_of(pstart + kk, tiles_m, tiles_n, g.xb, mt, nt);
+    mm0 = mt * BM;
+    nn0 = nt * BN;
+  };
+  auto issue = [&](int H, int mm0, int nn0) {
+    f16* dst = slot(H);
+    const int kofs = (H >> 2) * BK;
+    const int hh = H & 3;
+    if (hh < 2) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = (wid * 2 + i) * 8;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            b_rsrc, (lds_ptr_t)(dst + row * BK), 16,
+            b_voff + (int)(((int64_t)(nn0 + hh * 128 + row) * g.ldb + kofs) * 2), 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = (wid * 2 + i) * 8;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            a_rsrc, (lds_ptr_t)(dst + row * BK), 16,
+            a_voff + (int)(((int64_t)(mm0 + (hh - 2) * 128 + row) * g.lda + kofs) * 2), 0, 0, 0);
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+  const int fr = lane & 15, fg = lane >> 4;
+  const int foff0 = fr * BK + ((fg ^ (fr & 7)) << 3);
+  const int foff1 = fr * BK + (((4 + fg) ^ (fr & 7)) << 3);
+  const int a_row0 = 0, b_row0 = (wn & 1) * WTN;
+  auto read_a = [&](f16x8 (&af)[QTM], const f16* img, int mh, int foff) {
+#pragma unroll
+    for (int i = 0; i < QTM; ++i) af[i] = *(const f16x8*)(img + (a_row0 + mh * 64 + i * 16) * BK + foff);
+  };
+  auto read_b = [&](f16x8 (&bf)[TN], const f16* img, int foff) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bf[j] = *(const f16x8*)(img + (b_row0 + j * 16) * BK + foff);
+  };
+  auto mma = [&](const f16x8 (&af)[QTM], const f16x8 (&bf)[TN], int mh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < QTM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[mh * QTM + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[mh * QTM + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  const int nk = g.K / BK;  // >= 2
+  f16x8 fx[QTM], fy[QTM], fb0[TN], fb1[TN];
+  auto ktile = [&](int kt, auto mode_tag) {
+    constexpr int MODE = decltype(mode_tag)::value;
+    const int h0 = 4 * kt;
+    const f16* ia = slot(h0 + 2 + wm);
+    const f16* ib = slot(h0 + (wn >> 1));
+    read_a(fx, ia, 0, foff0);
+    read_b(fb0, ib, foff0);
+    if constexpr (MODE <= 1) issue(h0 + E, m0, n0);
+    lds_barrier();
+    mma(fx, fb0, 0);
+    lds_barrier();
+    read_a(fy, ia, 1, foff0);
+    if constexpr (MODE <= 1) issue(h0 + E + 1, m0, n0);
+    lds_barrier();
+    mma(fy, fb0, 1);
+    lds_barrier();
+    read_a(fx, ia, 1, foff1);
+    read_b(fb1, ib, foff1);
+    if constexpr (MODE == 0) issue(h0 + E + 2, m0, n0);
+    lds_barrier();
+    mma(fx, fb1, 1);
+    lds_barrier();
+    read_a(fy, ia, 0, foff1);
+    if constexpr (MODE == 0) {
+      issue(h0 + E + 3, m0, n0);
+      wait_vmcnt<2 * 2>();
+    } else if constexpr (MODE == 1) {
+      wait_vmcnt<0>();
+    }
+    lds_barrier();
+    mma(fy, fb1, 0);
+    lds_barrier();
+  };
+
+  tile_at(k, m0, n0);
+#pragma unroll
+  for (int h = 0; h < E; ++h) issue(h, m0, n0);
+  wait_vmcnt<2 * 2>();
+  lds_barrier();
+  if (wm == 1) lds_barrier();  // the stagger
+#pragma unroll 1
+  for (;;) {
+    f16x4 bv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU)
+        bv[j] = *(const f16x4*)(g.bias + n0 + wn * WTN + j * 16 + 4 * fg);
+      else
+        bv[j] = f16x4{};
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk - 2; ++kt) ktile(kt, std::integral_constant<int, 0>{});
+    ktile(nk - 2, std::integral_constant<int, 1>{});
+    ktile(nk - 1, std::integral_constant<int, 2>{});
+    if (wm == 0) lds_barrier();  // even out the barrier count: every wave is past its last ring read
+    const int kn = k + nl;
+    const bool more = kn < psize;
+    int m1 = 0, n1 = 0;
+    if (more) tile_at(kn, m1, n1);
+    if (more) {  // the next tile's prologue, under this tile's epilogue
+#pragma unroll
+      for (int h = 0; h < E; ++h) issue(h, m1, n1);
+    }
+    epilogue_staged8p<EPI>(g, lds + 6 * HALF, acc, bv, m0, n0, wm, wn, tid, fr, fg, c_rsrc, x_rsrc);
+    if (!more) break;
+    // the next tile's first K-tile: all but its last two half-tiles' loads and this epilogue's stores
+    if (EPI == EPI_BIAS_GELU && g.aux_out) wait_vmcnt<2 * 2 + 32>();
+    else wait_vmcnt<2 * 2 + 16>();
+    lds_barrier();
+    if (wm == 1) lds_barrier();  // the stagger
+    k = kn;
+    m0 = m1;
+    n0 = n1;
+  }
+}
+
+int launch_tile8f(const GemmArgs& a, int epi, hipStream_t st);
+
+int launch_tile8p(const GemmArgs& a, int epi, hipStream_t st) {
+  const int tiles = ((a.M + 255) / 256) * (a.N / 256);
+  const int grid = std::min(tiles, mf_cu_count()) / 8 * 8;
+  if (epi == EPI_F32 || !a.vec8 || a.N % 256 || grid < 8 || (int64_t)a.M * a.ldc * 2 >= (1ll << 31) ||
+      (int64_t)a.M * a.ld_aux * 2 >= (1ll << 31))
+    return mf_set_error("mf_gemm: persistent 256x256 tile needs fp16 C, N % 256 == 0, >= 8 tiles, < 2 GB", -2);
+  switch (epi) {
+    case EPI_NONE: gemm8p_kernel<EPI_NONE><<<grid, 512, 0, st>>>(a); break;
+    case EPI_BIAS: gemm8p_kernel<EPI_BIAS><<<grid, 512, 0, st>>>(a); break;
+    case EPI_BIAS_GELU: gemm8p_kernel<EPI_BIAS_GELU><<<grid, 512, 0, st>>>(a); break;
+    default: return launch_tile8f(a, epi, st);  // residual / QuickGELU' epilogues: gemm8f (bit-identical)
+  }
+  MF_CHECK_LAUNCH();
+  return 0;
+}
+
 int launch_tile8s(const GemmArgs& a, int epi, hipStream_t st) {
   const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
   dim3 grid(tiles), block(512);
@@ -1161,6 +1425,12 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
       // 735 / 663 on 160x128 / 256x256); r06: the eval engine's out-projection (M = 79 600 at EVAL_GROUP 4, N = K =
       // 768) 711..741 on 256x256 against 692..700 on 160x128 (profiles/r06_v1_gemm_eval4_*.txt, r06_v2_*)
       tile = (N >= 1536 || K >= 1024 || (N >= 768 && K >= 768)) ? 40 : 10;
+      // r06: >= 2 048 such tiles (>= 8 per CU) with an epilogue that reads no global operand run persistent
+      // (gemm8p: the next tile's prologue under this tile's epilogue, bit-identical): eval4 qkv 951 -> 975, fc 811
+      // -> 858, c5.qkv 789 -> 842, c5.dqkv 939 -> 954 TFLOP/s (profiles/r06_v7_gemm8p_*.txt)
+      if (tile == 40 && N % 256 == 0 && (int64_t)((M + 255) / 256) * (N / 256) >= 2048 &&
+          (epilogue == EPI_NONE || epilogue == EPI_BIAS || epilogue == EPI_BIAS_GELU))
+        tile = 41;
     else if (M >= 4096 && K >= 512)  // vision products (M = 6368), tests/diagnostics/gemm_bench.py:
       // N = 3072: 160x128 (960 tiles); N = 768: 96x128 (402 tiles, two workgroups per CU) for K >= 2048,
       // 160x64 (480 tiles) for K = 768; +6..37 % over the 128-row tiles
@@ -1181,7 +1451,7 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     } else
       tile = t128 >= 512 ? 1 : (t128 >= 256 ? 2 : 3);
   }
-  // tile ids: the ones the heuristic picks (1, 2, 3, 10, 15, 16, 26, 31, 33, 40 = gemm8f), plus 11 (160x128 with a
+  // tile ids: the ones the heuristic picks (1, 2, 3, 10, 15, 16, 26, 31, 33, 40 = gemm8f, 41 = gemm8p), plus 11 (160x128 with a
   // 3-stage ring), 20 (gemm8s, the [256][32]-image 256x256 kernel gemm8f replaced in r05), 21 (8-wave 256x128) and
   // 22 (the unstaggered gemm8 at 256x256) as A/B baselines (tests/diagnostics/gemm_bench.py); the sweep also covered
   // 128x192, 192x128, 128x160, 160x160, 224x128, 96x192, 64x128, 160x192, 192x192, 256x128 on 4 waves and 128x256 /
@@ -1205,6 +1475,7 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
     case 21: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 128, 2, 4>(a, epilogue, st);
     case 22: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8<256, 256, 2, 4>(a, epilogue, st);
     case 40: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8f(a, epilogue, st);
+    case 41: return K < 128 ? launch_tile<128, 128, 2, 2, 2>(a, epilogue, st) : launch_tile8p(a, epilogue, st);
     default: return mf_set_error("mf_gemm: bad tile id", -2);
   }
 }

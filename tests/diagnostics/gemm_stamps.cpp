@@ -3,11 +3,11 @@
 // K-tile landed, main loop done, epilogue done; plus its XCC id and HW_ID.  Prints the launch
 // span and per-phase distributions.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DMF_GEMM_STAMPS -I../../federated_multi_modal_amd/csrc \
-//         gemm_stamps.cpp -o gemm_stamps && ./gemm_stamps M N K epi tile
+//         gemm_stamps.cpp -o gemm_stamps && ./gemm_stamps M N K epi tile [aux_out]
+// aux_out 0: EPI_BIAS_GELU without the pre-activation store (the forward-only eval engine)
 #define MF_GEMM_STAMPS 1
 #include "../../federated_multi_modal_amd/csrc/common.hip"
 #include "../../federated_multi_modal_amd/csrc/gemm.hip"
-#include "../../federated_multi_modal_amd/csrc/blaslt.hip"
 
 #include <algorithm>
 #include <cstdio>
@@ -21,6 +21,7 @@ int main(int argc, char** argv) {
   if (tile == 2) BN = 64;
   if (tile == 3) BM = BN = 64;
   if (tile >= 20) { BM = tile == 23 || tile == 24 ? 128 : 256; BN = (tile == 20 || tile == 23 || tile >= 27) ? 256 : 128; }
+  const bool aux_out = argc > 6 ? atoi(argv[6]) != 0 : true;
   // tile 27 (persistent): one stamp row per TILE (start = its loop iteration), not per workgroup
   if (tile == 10) { BM = 160; BN = 128; }
   if (tile == 15) { BM = 96; BN = 128; }
@@ -40,7 +41,7 @@ int main(int argc, char** argv) {
   hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st));
   for (int rep = 0; rep < 5; ++rep) {
     hipMemset(st, 0, (size_t)tiles * 64);
-    int rc = mf_gemm_nt(A, K, B, K, C, N, M, N, K, bias, aux, aux, N, epi, tile, 0);
+    int rc = mf_gemm_nt(A, K, B, K, C, N, M, N, K, bias, aux, aux_out ? aux : nullptr, N, epi, tile, 0);
     if (rc) { printf("error %s\n", mf_last_error()); return 1; }
     hipDeviceSynchronize();
   }

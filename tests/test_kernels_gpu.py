@@ -73,6 +73,32 @@ def test_gemm8_fullline_matches_staggered(dev, M, N, K):
                 assert torch.equal(outs[0][1], aux_out), f"epilogue {epi}, variant {k} (pre-activation)"
 
 
+@pytest.mark.parametrize("M,N,K", [(79600, 2304, 768), (19900, 768, 3072), (3000, 512, 128), (77000, 512, 512)])
+def test_gemm8p_persistent_matches_gemm8f(dev, M, N, K):
+    """The persistent 256x256 kernel gemm8p (tile 41: one workgroup per CU walking its XCD's tiles, the next tile's
+    prologue under this tile's register-direct epilogue) against gemm8f (tile 40) -- bit-identical for every fp16
+    epilogue, ragged M included, with and without the pre-activation store."""
+    g = torch.Generator(device="cpu").manual_seed(M + K + 1)
+    A = torch.randn(M, K, generator=g).half().to(dev)
+    B = (torch.randn(N, K, generator=g) * K ** -0.5).half().to(dev)
+    b = (torch.randn(N, generator=g) * 0.1).half().to(dev)
+    R = torch.randn(M, N, generator=g).half().to(dev)
+    for epi in (ops.EPI_NONE, ops.EPI_BIAS, ops.EPI_BIAS_RESID, ops.EPI_BIAS_GELU, ops.EPI_DGELU, ops.EPI_RESID):
+        kw = {"bias": b} if epi in (ops.EPI_BIAS, ops.EPI_BIAS_RESID, ops.EPI_BIAS_GELU) else {}
+        aux_in = R if epi in (ops.EPI_BIAS_RESID, ops.EPI_DGELU, ops.EPI_RESID) else None
+        for with_aux_out in ((True, False) if epi == ops.EPI_BIAS_GELU else (False,)):
+            outs = []
+            for tile in (40, 41):
+                aux_out = torch.full((M, N), 3.0, device=dev, dtype=torch.float16) if with_aux_out else None
+                C = torch.full((M, N), 5.0, device=dev, dtype=torch.float16)
+                ops.gemm_nt(A, B, C=C, aux_in=aux_in, aux_out=aux_out, epilogue=epi, tile=tile, **kw)
+                outs.append((C, aux_out))
+            torch.cuda.synchronize()
+            assert torch.equal(outs[0][0], outs[1][0]), f"epilogue {epi}, aux_out {with_aux_out}"
+            if with_aux_out:
+                assert torch.equal(outs[0][1], outs[1][1]), f"epilogue {epi} (pre-activation)"
+
+
 @pytest.mark.parametrize("M,N,K,epi", [(2926, 512, 2048, 2), (2926, 1536, 512, 1), (6368, 768, 3072, 0),
                                        (6368, 3072, 768, 3), (6368, 768, 768, 4), (770, 512, 512, 0)])
 def test_gemm_side_tower_tile_hint_is_bit_identical(dev, M, N, K, epi):
