@@ -1425,12 +1425,10 @@ extern "C" int mf_gemm(const void* A, int64_t lda, int a_kmajor, const void* B, 
       // 735 / 663 on 160x128 / 256x256); r06: the eval engine's out-projection (M = 79 600 at EVAL_GROUP 4, N = K =
       // 768) 711..741 on 256x256 against 692..700 on 160x128 (profiles/r06_v1_gemm_eval4_*.txt, r06_v2_*)
       tile = (N >= 1536 || K >= 1024 || (N >= 768 && K >= 768)) ? 40 : 10;
-      // r06: >= 2 048 such tiles (>= 8 per CU) with an epilogue that reads no global operand run persistent
-      // (gemm8p: the next tile's prologue under this tile's epilogue, bit-identical): eval4 qkv 951 -> 975, fc 811
-      // -> 858, c5.qkv 789 -> 842, c5.dqkv 939 -> 954 TFLOP/s (profiles/r06_v7_gemm8p_*.txt)
-      if (tile == 40 && N % 256 == 0 && (int64_t)((M + 255) / 256) * (N / 256) >= 2048 &&
-          (epilogue == EPI_NONE || epilogue == EPI_BIAS || epilogue == EPI_BIAS_GELU))
-        tile = 41;
+      // r06: the persistent gemm8p (tile 41) is faster isolated on these launches (eval4 qkv 951 -> 975, fc 811 ->
+      // 858, c5.qkv 789 -> 842 TFLOP/s, profiles/r06_v7_gemm8p_*.txt) but slower in the engine: eval pass 22 700 ->
+      // 20 900 img/s, C5 1 261 -> 1 145 img/s (same box, interleaved, profiles/r06_v8_gemm8p_engine_ab.txt), so
+      // it is not routed
     else if (M >= 4096 && K >= 512)  // vision products (M = 6368), tests/diagnostics/gemm_bench.py:
       // N = 3072: 160x128 (960 tiles); N = 768: 96x128 (402 tiles, two workgroups per CU) for K >= 2048,
       // 160x64 (480 tiles) for K = 768; +6..37 % over the 128-row tiles
