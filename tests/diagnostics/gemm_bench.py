@@ -11,9 +11,13 @@ each tile configuration against a torch fp32 matmul.  Prints TFLOP/s.
                                         eval4: the eval engine's launches at EVAL_GROUP 4 (400 images, 79 600
                                         rows); in both eval sets c_fc stores no pre-activation (forward-only engine)
 
+GEMM_BENCH_REPS (default 20) sets the launches per timed hipGraph (300 holds each kernel ~10-30 ms,
+long enough for the clock to settle to the sustained-load level the engine sees).
+
 A "!" marks a tile whose plain product misses the fp32 reference, "~" one whose output (with the
 shape's epilogue) is not bit-identical to the first listed tile's.
 """
+import os
 import sys
 from pathlib import Path
 
@@ -38,7 +42,7 @@ SHAPES = [  # (name, M, N, K, epilogue, calls per c4 step)
 ROUNDS = 3
 
 
-def timeit(fn, reps=20):
+def timeit(fn, reps=int(os.environ.get("GEMM_BENCH_REPS", "20"))):
     """Kernel time per call: `reps` calls captured in one hipGraph and replayed (no host overhead)."""
     for _ in range(3):
         fn()
