@@ -292,8 +292,9 @@ __global__ __launch_bounds__(HWB * 32) void ln_bwd2_kernel(const f16* __restrict
   // (compact row (v / seg_full) * seg_live + v % seg_full); the rest are rows whose dy is exactly zero (the text
   // tower's tokens after every class's EOT, mf_layernorm_bwd_live): they add nothing, so the row blocks, and with
   // them the dgamma / dbeta partials, are those of the full-length tower.  A dead row's loads still run (from
-  // compact row 0, a cache hit) so that the load / wait structure is the plain kernel's: r05 measured a version
-  // that branched around them giving run-to-run different dgamma partials under tower concurrency.
+  // compact row 0, a cache hit) so that the load / wait structure is the plain kernel's.  (r05 saw a version that
+  // branched around them give run-to-run different dgamma partials under tower concurrency; r06 traced that to the
+  // packed fp32 VALU path, which the library no longer builds with -- DESIGN.md §6, tests/test_isa.py.)
   constexpr int CH = D / 256;
   static_assert(HWB == 8 || HWB == 16, "half-waves per block");
   constexpr int RPH = LN_ROWS_PER_BLOCK / HWB;  // rows per half-wave

@@ -50,5 +50,8 @@ for rows, D in [(6368, 768), (2926, 512), (796, 768), (770, 512)]:
     err = (y.float() - ref).abs().max().item()
     ck = (y.view(torch.int16).long().sum().item(), dx.view(torch.int16).long().sum().item(), dg.double().sum().item())
     bf, bb = 4.0 * rows * D, 8.0 * rows * D
-    print(f"rows={rows} D={D}: fwd {tf:6.2f} us {bf / tf / 1e3:6.0f} GB/s | bwd {tb:6.2f} us {bb / tb / 1e3:6.0f} GB/s"
-          f" | max err {err:.2e} ck {ck}", flush=True)
+    # same-traffic streaming yardsticks: a copy (fwd's read + write) and addcmul (bwd's three reads + write)
+    tc = timeit(lambda: y.copy_(x))
+    ta = timeit(lambda: torch.addcmul(x, dy, dres, out=dx))
+    print(f"rows={rows} D={D}: fwd {tf:6.2f} us {bf / tf / 1e3:6.0f} GB/s (copy {tc:6.2f} us) | bwd {tb:6.2f} us "
+          f"{bb / tb / 1e3:6.0f} GB/s (addcmul {ta:6.2f} us) | max err {err:.2e} ck {ck}", flush=True)
