@@ -453,6 +453,30 @@ def main():
 
     eval_full, eval_cached = eval_rate(False), eval_rate(True)
 
+    # the engine test() itself runs (trainers.MaPLe.test): forward-only (EngineConfig.inference), TRAINER.MAPLE.
+    # EVAL_GROUP (4) x TEST.BATCH_SIZE (100) images per launch, the text features encoded by the first launch of
+    # the pass; each launch copies its 400 images into the engine's input buffer as test() does
+    def eval_rate_test_engine(images=400, n=6):
+        import dataclasses
+        ev = MapleEngine(dataclasses.replace(eng.cfg, batch=images, inference=True), device=dev, shared=eng)
+        reps = -(-images // B)
+        imgs = torch.cat([batches[i % 2][0] for i in range(reps)])[:images].contiguous()
+        labs = torch.cat([batches[i % 2][1] for i in range(reps)])[:images].contiguous()
+        ev.img_in.copy_(imgs)
+        ev.eval_batch(labs, acc)
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for _ in range(n):
+            ev.img_in.copy_(imgs)
+            ev.eval_batch(labs, acc, reuse_text=True)
+        torch.cuda.synchronize()
+        rate = images * n / (time.perf_counter() - a)
+        del ev
+        torch.cuda.empty_cache()
+        return rate
+
+    eval_test_engine = eval_rate_test_engine()
+
     # ---------------- FedAvg overlapped with the client's last local test() (trainers/maple.py:646; the
     # trainer starts the exchange there, MaPLeFederated.train): exposed = (pack + exchange started, test
     # pass, wait + unpack) - (test pass alone), max over ranks, median of 3
@@ -667,7 +691,10 @@ def main():
         "caption_mode": cap_mode,
         "c5_side": c5,
         "eval_images_per_s": {"text_reencoded_per_batch": eval_full, "text_cached_per_pass": eval_cached,
-                              "per_gpu": True},
+                              "test_engine_group4_per_pass": eval_test_engine, "per_gpu": True,
+                              "note": "text_* fields: the training engine's forward at its B-image batch; "
+                                      "test_engine_group4_per_pass: the forward-only engine test() runs, 400 "
+                                      "images (EVAL_GROUP 4 x TEST.BATCH_SIZE 100) per launch, text cached"},
         "input_transform": input_transform,
         "model_tflops": world * step_flop * args.steps / elapsed / 1e12,
         "model_mfma_frac": world * step_flop * args.steps / elapsed / MFMA_PEAK_F16 / world,
