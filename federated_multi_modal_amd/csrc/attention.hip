@@ -152,9 +152,12 @@ MF_DEV void fwd4_tile(const f16* sK, const f16* sV, const int* koff, const int* 
       // exceed the 128-VGPR budget of 16 waves per CU)
       if (ks & 1) asm volatile("" ::: "memory");
     }
+    // every launch stages LKP = L rounded up to 16 keys (mf_attention_fwd / _rows), so L > LKP - 16: without the
+    // causal mask only the chunks reaching past LKP - 16 can hold keys >= L, and the others skip the key test at
+    // compile time
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      if (ks < ks_end && (CAUSAL || 32 * ks + 32 > L)) {
+      if (ks < ks_end && (CAUSAL || (32 * ks + 32 > LKP - 15 && 32 * ks + 32 > L))) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int key0 = 32 * ks + 4 * fg + i, key1 = key0 + 16;
