@@ -243,6 +243,8 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (K=1000 text side) side metric")
     ap.add_argument("--no-caption-mode", action="store_true", help="skip the caption-batch (K19) side metric")
     ap.add_argument("--no-round", action="store_true", help="skip the FedAvg round wall-time (trainer) runs")
+    ap.add_argument("--no-eval", action="store_true",
+                    help="skip the eval-rate side metrics (keeps a kernel profile of the run to the training step's mix)")
     # engine options (EngineConfig; results bit-identical, for same-box A/B: scripts/bench_ab.sh)
     ap.add_argument("--fused-qkv-attn", default="side", choices=["side", "none", "both", "vision", "text"])
     ap.add_argument("--text-first", action="store_true", help="enqueue the text tower first after each fork")
@@ -451,7 +453,7 @@ def main():
         torch.cuda.synchronize()
         return B * n / (time.perf_counter() - a)
 
-    eval_full, eval_cached = eval_rate(False), eval_rate(True)
+    eval_full, eval_cached = (None, None) if args.no_eval else (eval_rate(False), eval_rate(True))
 
     # the engine test() itself runs (trainers.MaPLe.test): forward-only (EngineConfig.inference), TRAINER.MAPLE.
     # EVAL_GROUP (4) x TEST.BATCH_SIZE (100) images per launch, the text features encoded by the first launch of
@@ -475,7 +477,7 @@ def main():
         torch.cuda.empty_cache()
         return rate
 
-    eval_test_engine = eval_rate_test_engine()
+    eval_test_engine = None if args.no_eval else eval_rate_test_engine()
 
     # ---------------- FedAvg overlapped with the client's last local test() (trainers/maple.py:646; the
     # trainer starts the exchange there, MaPLeFederated.train): exposed = (pack + exchange started, test

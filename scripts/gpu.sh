@@ -27,7 +27,7 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-QUICK="--no-cpu-baseline --no-round --no-eot-mode --no-c5 --no-caption-mode"
+QUICK="--no-cpu-baseline --no-round --no-eot-mode --no-c5 --no-caption-mode --no-eval"
 
 step() {
   case "$1" in
