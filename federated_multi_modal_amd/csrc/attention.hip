@@ -238,12 +238,23 @@ __global__ __launch_bounds__(MAXT) void attn_fwd4_kernel(const f16* __restrict__
   __shared__ __attribute__((aligned(16))) f16 sK[LKP * 64];
   __shared__ __attribute__((aligned(16))) f16 sV[LKP * 64];
   const int D = H * 64;
-  const int nh = blockIdx.x, n = nh / H, h = nh % H;
+  // (head, query split) of this workgroup.  257..512 rows (MAXT = 512, one workgroup per CU) with the heads a
+  // multiple of 8: the gridDim.y splits of a head take dispatch ids 8 apart (the hardware deals consecutive ids
+  // round-robin to the 8 XCDs), so they run on one XCD at the same time and the second staging of the head's K / V
+  // finds it in that XCD's L2 (r06, tests/diagnostics/attn_bench.py: 455 rows 50 -> 45 us; at c4's 199 rows the
+  // same pairing is slower, 13.8 -> 14.4 us, profiles/r06_v17_attn_split_pairing.txt)
+  int nh = blockIdx.x, split = blockIdx.y;
+  if (MAXT == 512 && gridDim.y > 1 && (gridDim.x & 7) == 0) {
+    const int id = blockIdx.x + blockIdx.y * gridDim.x, per = 8 * gridDim.y;
+    nh = (id / per) * 8 + (id & 7);
+    split = (id % per) >> 3;
+  }
+  const int n = nh / H, h = nh % H;
   const f16* base = qkv + (int64_t)n * L * ld_qkv;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int fr = lane & 15, fg = lane >> 4, ii = lane & 15;
   const int qstep = gridDim.y * nw * 16;
-  int q0 = (blockIdx.y * nw + w) * 16;
+  int q0 = (split * nw + w) * 16;
   const bool active = q0 < Lq;
   MF_ASTAMP2(0);
   f16x8 qf0, qf1;
