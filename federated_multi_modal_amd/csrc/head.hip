@@ -43,7 +43,7 @@ __global__ void logits_kernel(const f16* __restrict__ img_n, const f16* __restri
     const float sc = fminf(expf(logit_scale[0]), 100.f);
     const float m16 = r16(s);
     mm[w] = (f16)m16;
-    logits[w] = (f16)(sc * m16);
+    logits[w] = (f16)mul32(sc, m16);  // fp32 product, then fp16 (mf_common.h mul32)
   }
 }
 
@@ -79,7 +79,7 @@ __global__ void loss_kernel(const f16* __restrict__ logits, const f16* __restric
       const float g_nll = (k == y) ? r16(-1.0f / (float)B) : 0.f;
       // log_softmax backward: g - exp(out) * sum(g)
       const float dl = r16(g_nll - expf(logp) * r16(-1.0f / (float)B));
-      dmm[(int64_t)b * K + k] = (f16)(dl * sc);
+      dmm[(int64_t)b * K + k] = (f16)mul32(dl, sc);
     }
     // cosine similarity of img_n[b] and txt_n[y]
     float su = 0.f, sv = 0.f;
@@ -267,7 +267,7 @@ __global__ void loss_soft_kernel(const f16* __restrict__ logits, const f16* __re
       const float logp = r16((float)lr[k] - mx - lse);
       const float g = r16(-fmaxf(qr[k], 1e-8f) * invB);
       const float dl = r16(g - expf(logp) * sg);
-      dmm[(int64_t)b * K + k] = (f16)(dl * sc);
+      dmm[(int64_t)b * K + k] = (f16)mul32(dl, sc);
     }
     const f16* tr = tgt + (int64_t)b * D;
     const f16* ir = img_n + (int64_t)b * D;

@@ -33,8 +33,24 @@ MF_DEV float wave_max(float v) {
 // QuickGELU with the reference's three fp16 roundings (clip/model.py:162-164):
 //   t1 = fp16(1.702*f); t2 = fp16(sigmoid(t1)); g = fp16(f*t2)
 // sigmoid in fp32 with the hardware reciprocal (v_rcp_f32, 1 ulp): its result is rounded to fp16
-// next, so the fp32 ulp matters only within 2^-13 of an fp16 rounding boundary
+// next, so the fp32 ulp matters only within 2^-13 of an fp16 rounding boundary.  t1 and the backward's
+// fp16(dt1*1.702) are left to the compiler's v_fma_mixlo_f16, which rounds the exact product once (the
+// reference: fp32 product, then fp16): 61 of the 61 094 finite fp16 f give a t1 one fp16 ulp away.  r06 measured the
+// reference's two roundings there (mul32 below): logits moved both ways (c3_j9_k10_b4: max |err| vs the reference
+// 2.93e-3 -> 4.88e-3 against a 4.0e-3 gate, vs fp64 3.5e-3 -> 2.5e-3), so the gated form stays.
 MF_DEV float sigmoid32(float t) { return __builtin_amdgcn_rcpf(1.0f + __expf(-t)); }
+
+// fp32 product of a and b, materialised as fp32 before any fp16 rounding of it: the reference's fp16 op rounds its
+// fp32 opmath product to fp16 (two roundings), while the compiler folds fp16(a * b) into v_fma_mixlo_f16, which
+// rounds the exact product once -- a different fp16 for 61 of the 61 094 finite fp16 inputs of f * 1.702f
+// (r06, tests/diagnostics/mixround/).  Products of two fp16 values are exact in fp32 and need no barrier.  Used
+// where an fp16 tensor meets an fp32 scalar at the head and in the optimizer (logit scale, clip coefficient,
+// momentum).
+MF_DEV float mul32(float a, float b) {
+  float p = a * b;
+  asm volatile("" : "+v"(p));
+  return p;
+}
 
 MF_DEV float quick_gelu16(float f, float* t2_out) {
   float t1 = r16(f * 1.702f);

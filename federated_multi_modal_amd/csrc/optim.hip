@@ -159,14 +159,14 @@ __global__ void sgd_kernel(T* __restrict__ p, T* __restrict__ g, T* __restrict__
   const float lr = hyper[0], momentum = hyper[1], wd = hyper[2];
   const bool first = hyper[3] != 0.f;
   const float pv = (float)p[i];
-  const float gc = (float)(T)((float)g[i] * coef);
+  const float gc = (float)(T)mul32((float)g[i], coef);
   g[i] = (T)gc;
   const float dp = (float)(T)(gc + wd * pv);
   float b;
   if (first)
     b = dp;
   else
-    b = (float)(T)((float)(T)((float)buf[i] * momentum) + dp);
+    b = (float)(T)((float)(T)mul32((float)buf[i], momentum) + dp);
   buf[i] = (T)b;
   p[i] = (T)(pv + (-lr) * b);
 }
@@ -185,14 +185,14 @@ MF_DEV void sgd8_body(T* __restrict__ p, T* __restrict__ g, T* __restrict__ buf,
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const float pe = (float)pv[e];
-    const float gc = (float)(T)((float)gv[e] * coef);
+    const float gc = (float)(T)mul32((float)gv[e], coef);
     gv[e] = (T)gc;
     const float dp = (float)(T)(gc + wd * pe);
     float b;
     if (first)
       b = dp;
     else
-      b = (float)(T)((float)(T)((float)bv[e] * momentum) + dp);
+      b = (float)(T)((float)(T)mul32((float)bv[e], momentum) + dp);
     bv[e] = (T)b;
     pv[e] = (T)(pe + (-lr) * b);
   }
